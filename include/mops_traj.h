@@ -1,0 +1,194 @@
+/*
+ * mops_traj.h -- C ABI of the MI355X (gfx950) particle-trajectory engine.
+ *
+ * Drop-in boundary for the reference's trajectory path (YosefQiu/MOPS):
+ * every entry point below replaces one reference interface, cited per
+ * function.  Plain pointers and sizes only; no C++ or torch types.  Device
+ * pointers are named d_*, host pointers h_*; `stream` is a hipStream_t
+ * passed as void* (NULL = the default stream).
+ *
+ * Conventions taken from the reference so a caller can pass its own arrays
+ * unchanged:
+ *   - connectivity is size_t (uint64_t), 1-based, 0 = missing
+ *     (MPASOGrid::verticesOnCell_vec / cellsOnCell_vec / cellsOnVertex_vec,
+ *     src/Core/MPASOGrid.h);
+ *   - coordinates are AoS xyz doubles (std::vector<vec3>::data());
+ *   - fields are row-major [entity][level] (MPASOSolution vectors).
+ * Internally the engine keeps its own int32 0-based, per-cell-record layout
+ * in HBM.
+ *
+ * Error convention: every function returns mops_status.  MOPS_ERR_INVALID
+ * is what the reference answers with Error() + an empty result
+ * (MPASOVisualizerKernels.cpp:659-669); mops_last_error() gives the text.
+ * Per-particle failures are not errors: the particle stops ("dies") exactly
+ * where the reference's lambda returns, and its death step is reported.
+ */
+#ifndef MOPS_TRAJ_H
+#define MOPS_TRAJ_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef enum {
+    MOPS_OK = 0,
+    MOPS_ERR_INVALID = -1,     /* bad arguments / settings (reference: Error() + {}) */
+    MOPS_ERR_HIP = -2,         /* HIP runtime failure */
+    MOPS_ERR_UNSUPPORTED = -3  /* e.g. maxEdges > 20 (reference MAX_VERTEX_NUM) */
+} mops_status;
+
+/* CalcDirection / CalcMethodType (src/Core/MPASOVisualizer.h:14-15) */
+enum { MOPS_FORWARD = 0, MOPS_BACKWARD = 1 };
+enum { MOPS_RK4 = 0, MOPS_EULER = 1 };
+
+typedef struct mops_mesh mops_mesh;    /* device-resident mesh (opaque) */
+typedef struct mops_field mops_field;  /* device-resident derived snapshot (opaque) */
+
+/* Host description of an MPAS-O mesh, in MPASOGrid's storage form. */
+typedef struct {
+    int64_t n_cells;                     /* mCellsSize */
+    int64_t n_vertices;                  /* mVertexSize */
+    int32_t max_edges;                   /* mMaxEdgesSize */
+    int32_t n_vert_levels;               /* mVertLevels (the w grid has +1) */
+    const uint64_t* h_n_edges_on_cell;   /* numberVertexOnCell_vec [C] */
+    const uint64_t* h_vertices_on_cell;  /* verticesOnCell_vec [C*maxE] */
+    const uint64_t* h_cells_on_cell;     /* cellsOnCell_vec [C*maxE] */
+    const uint64_t* h_cells_on_vertex;   /* cellsOnVertex_vec [V*3] */
+    const double* h_cell_coord;          /* cellCoord_vec [C*3] */
+    const double* h_vertex_coord;        /* vertexCoord_vec [V*3] */
+} mops_mesh_desc;
+
+/* Raw per-cell fields of one history snapshot (MPASOSolution members). */
+typedef struct {
+    int32_t timestep;                    /* mTimesteps (informational) */
+    const double* h_layer_thickness;     /* cellLayerThickness_vec [C*L] (required) */
+    const double* h_bottom_depth;        /* cellBottomDepth_vec [C] or NULL */
+    const double* h_surface_height;      /* cellSurfaceHeight_vec [C] or NULL */
+    const double* h_zonal_velocity;      /* cellZonalVelocity_vec [C*L] */
+    const double* h_meridional_velocity; /* cellMeridionalVelocity_vec [C*L] */
+    const double* h_vert_velocity_top;   /* cellVertVelocity_vec [C*(L+1)] or NULL (= 0) */
+} mops_snapshot_desc;
+
+/* TrajectorySettings (src/Core/MPASOVisualizer.h:90-103); seconds. */
+typedef struct {
+    int64_t delta_t;                     /* deltaT */
+    int64_t simulation_duration;         /* simulationDuration */
+    int64_t record_t;                    /* recordT */
+    int32_t direction;                   /* MOPS_FORWARD / MOPS_BACKWARD */
+    int32_t method;                      /* MOPS_RK4 / MOPS_EULER (reference default Euler) */
+} mops_traj_cfg;
+
+/* Device-resident particle state, SoA, caller-owned (n entries each). */
+typedef struct {
+    int64_t n;
+    double* d_x;                         /* stable_points x,y,z (updated in place) */
+    double* d_y;
+    double* d_z;
+    float* d_depth;                      /* effective_depths (float, as the reference) */
+    int32_t* d_cell;                     /* in: seed cell (default_cell_id), then current cell */
+    int32_t* d_death_step;               /* out: -1 alive, else the step it died at */
+} mops_particles;
+
+const char* mops_last_error(void);
+int32_t mops_abi_version(void);
+
+/* ---- mesh / snapshots -------------------------------------------------- */
+
+/* Upload + re-layout a mesh.  Replaces MOPSApp::addGrid / MPASOGrid
+ * (src/Core/MOPSApp.cpp:65-75): the KD-tree build becomes the engine's
+ * bucket index for mops_locate_cells. */
+mops_status mops_mesh_create(const mops_mesh_desc* desc, void* stream, mops_mesh** out);
+void mops_mesh_destroy(mops_mesh* mesh);
+/* Bytes the mesh occupies in HBM. */
+int64_t mops_mesh_bytes(const mops_mesh* mesh);
+
+/* Upload raw fields and derive, on the GPU, the vertex arrays the trajectory
+ * kernels read.  Replaces MOPSApp::addSol's preprocessing chain
+ * (src/Core/MOPSApp.cpp:100-129): MPASOSolution::calcCellCenterZtop
+ * (MPASOSolution.cpp:535-618), TBBBackend::CalcCellVertexZtop
+ * (MPASOSolutionTBB.cpp:9-55), CalcCellCenterVelocityByZM (:108-129),
+ * CalcCellVertexVelocity (:270-318), CalcCellVertexVertVelocity (:320-366). */
+mops_status mops_field_create(const mops_mesh* mesh, const mops_snapshot_desc* desc, void* stream,
+                              mops_field** out);
+/* Upload already-derived vertex arrays (cellVertexZTop_vec [V*L],
+ * cellVertexVelocity_vec [V*L*3], cellVertexVertVelocity_vec [V*(L+1)]);
+ * the path MOPSApp::addSol takes when they are pre-set (MOPSApp.cpp:100,107,117). */
+mops_status mops_field_create_derived(const mops_mesh* mesh, const double* h_vertex_ztop,
+                                      const double* h_vertex_vel, const double* h_vertex_w,
+                                      void* stream, mops_field** out);
+/* Copy the derived vertex arrays back to the host (any pointer may be NULL). */
+mops_status mops_field_export(const mops_field* field, double* h_vertex_ztop, double* h_vertex_vel,
+                              double* h_vertex_w, void* stream);
+/* CalcCellCenterToVertex (MPASOSolutionTBB.cpp:57-106) for one double
+ * attribute [C*L] -> [V*L] (negative results clamped to 0), device pointers. */
+mops_status mops_cell_to_vertex_attr(const mops_mesh* mesh, const double* d_cell_attr, double* d_vertex_attr,
+                                     void* stream);
+void mops_field_destroy(mops_field* field);
+int64_t mops_field_bytes(const mops_field* field);
+
+/* ---- seed location ----------------------------------------------------- */
+
+/* Exact nearest cell centre (Euclidean) for n points [n*3] (device
+ * pointers).  Replaces MPASOField::calcInWhichCells -> MPASOGrid::searchKDT
+ * (src/Core/MPASOField.cpp:23-34, src/Core/MPASOGrid.cpp:287-313, nanoflann
+ * 1-NN).  Ties resolve to the smallest cell index. */
+mops_status mops_locate_cells(const mops_mesh* mesh, int64_t n, const double* d_points, int32_t* d_cells,
+                              void* stream);
+
+/* ---- trajectory hot path (device-resident) ----------------------------- */
+
+/* Number of record slots K = simulation_duration / record_t (reference
+ * each_points_size, MPASOVisualizerKernels.cpp:703). */
+int64_t mops_traj_num_records(const mops_traj_cfg* cfg);
+/* Number of integration steps = simulation_duration / delta_t. */
+int64_t mops_traj_num_steps(const mops_traj_cfg* cfg);
+
+/* Advance particles over global steps [step_begin, step_end) of one
+ * StreamLine (back == NULL; Kernel::StreamLine, MPASOVisualizerKernels.cpp:
+ * 874-1003) or PathLine (Kernel::PathLine, :1329-1483) call.  Records go to
+ * d_records laid out [K][6][record_stride] doubles (px,py,pz,vx,vy,vz);
+ * slot 0 also receives the seed / first-step velocity pre-writes
+ * (:901, :990).  The caller zero-fills d_records before step 0 (the
+ * reference's vector::resize zero-init).  Calling it over consecutive step
+ * ranges is identical to one call over [0, n_steps). */
+mops_status mops_traj_advance(const mops_mesh* mesh, const mops_field* front, const mops_field* back,
+                              const mops_traj_cfg* cfg, const mops_particles* particles,
+                              int64_t step_begin, int64_t step_end, double* d_records,
+                              int64_t record_stride, void* stream);
+
+/* FinalizeTrajectoryLines[WithAttrs] + RemoveNaNTrajectoriesAndReindex
+ * (src/Common/TrajectoryCommon.h:57-190) on the device: seeds [n*3] and
+ * records -> points/velocity [n*(K+1)*3], temperature/salinity [n*(K+1)]
+ * (pathline: velocity x/y, reference quirk Q9; streamline: zeros),
+ * last point [n*3].  Any output pointer except points may be NULL. */
+mops_status mops_traj_finalize(int64_t n, int64_t K, const double* d_seeds, const double* d_records,
+                               int64_t record_stride, int32_t pathline, double* d_points, double* d_velocity,
+                               double* d_temperature, double* d_salinity, double* d_last_point, void* stream);
+
+/* RemoveNaNTrajectoriesAndReindex alone on n lines of P points each, in
+ * place (device pointers; [n*P*3], [n*P*3], [n*P], [n*P], out [n*3]). */
+mops_status mops_remove_nan_lines(int64_t n, int64_t P, double* d_points, double* d_velocity,
+                                  double* d_temperature, double* d_salinity, double* d_last_point, void* stream);
+
+/* ---- host convenience (the backend plug point) ------------------------- */
+
+/* MOPS::Factory::StreamLine / PathLine (src/Common/MOPSFactory.h:27-39)
+ * with host buffers: seeds [n*3]; depths [n] or NULL (then `depth` for all,
+ * BuildEffectiveDepths, TrajectoryCommon.h:29-41); cells [n] in/out or NULL
+ * (entries < 0 are located, as default_cell_id); outputs as
+ * mops_traj_finalize plus the final positions (the caller's
+ * sample_points update in MOPSApp::runPathLine, MOPSApp.cpp:287-290) and
+ * death steps.  Any output pointer except h_points may be NULL. */
+mops_status mops_run_trajectories(const mops_mesh* mesh, const mops_field* front, const mops_field* back,
+                                  const mops_traj_cfg* cfg, int64_t n, const double* h_seeds,
+                                  const float* h_depths, float depth, int32_t* h_cells, double* h_points,
+                                  double* h_velocity, double* h_temperature, double* h_salinity,
+                                  double* h_last_point, double* h_final_pos, float* h_final_depth,
+                                  int32_t* h_death_step, void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* MOPS_TRAJ_H */

@@ -1,0 +1,100 @@
+"""ctypes binding of the C ABI in include/mops_traj.h (libmops_traj.so).
+
+This is the Python side of the drop-in boundary.  There is deliberately no
+fallback: if the HIP library is missing the import of any engine entry point
+raises, so a GPU box never silently runs something else.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "lib", "libmops_traj.so")
+
+# every symbol include/mops_traj.h declares (checked by tests/test_abi.py)
+EXPORTED = (
+    "mops_last_error", "mops_abi_version",
+    "mops_mesh_create", "mops_mesh_destroy", "mops_mesh_bytes",
+    "mops_field_create", "mops_field_create_derived", "mops_field_export", "mops_cell_to_vertex_attr",
+    "mops_field_destroy", "mops_field_bytes",
+    "mops_locate_cells",
+    "mops_traj_num_records", "mops_traj_num_steps", "mops_traj_advance", "mops_traj_finalize",
+    "mops_remove_nan_lines", "mops_run_trajectories",
+)
+
+MOPS_OK, MOPS_ERR_INVALID, MOPS_ERR_HIP, MOPS_ERR_UNSUPPORTED = 0, -1, -2, -3
+MOPS_FORWARD, MOPS_BACKWARD = 0, 1
+MOPS_RK4, MOPS_EULER = 0, 1
+
+
+class MeshDesc(C.Structure):
+    _fields_ = [("n_cells", C.c_int64), ("n_vertices", C.c_int64), ("max_edges", C.c_int32),
+                ("n_vert_levels", C.c_int32), ("h_n_edges_on_cell", C.c_void_p),
+                ("h_vertices_on_cell", C.c_void_p), ("h_cells_on_cell", C.c_void_p),
+                ("h_cells_on_vertex", C.c_void_p), ("h_cell_coord", C.c_void_p), ("h_vertex_coord", C.c_void_p)]
+
+
+class SnapshotDesc(C.Structure):
+    _fields_ = [("timestep", C.c_int32), ("h_layer_thickness", C.c_void_p), ("h_bottom_depth", C.c_void_p),
+                ("h_surface_height", C.c_void_p), ("h_zonal_velocity", C.c_void_p),
+                ("h_meridional_velocity", C.c_void_p), ("h_vert_velocity_top", C.c_void_p)]
+
+
+class TrajCfg(C.Structure):
+    _fields_ = [("delta_t", C.c_int64), ("simulation_duration", C.c_int64), ("record_t", C.c_int64),
+                ("direction", C.c_int32), ("method", C.c_int32)]
+
+
+class Particles(C.Structure):
+    _fields_ = [("n", C.c_int64), ("d_x", C.c_void_p), ("d_y", C.c_void_p), ("d_z", C.c_void_p),
+                ("d_depth", C.c_void_p), ("d_cell", C.c_void_p), ("d_death_step", C.c_void_p)]
+
+
+class MopsError(RuntimeError):
+    pass
+
+
+_lib = None
+
+
+def load(path: str | None = None):
+    """Load libmops_traj.so; raise loudly if it has not been built."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    path = path or LIB_PATH
+    if not os.path.exists(path):
+        raise MopsError(f"HIP engine library not found at {path}: run `python -c \"import __graft_entry__ as g; "
+                        f"g.build()\"` (hipcc --offload-arch=gfx950) first")
+    lib = C.CDLL(path)
+    P, I64, I32 = C.c_void_p, C.c_int64, C.c_int32
+    st = C.c_int
+    lib.mops_last_error.restype = C.c_char_p
+    lib.mops_abi_version.restype = I32
+    lib.mops_mesh_create.argtypes = [P, P, P]; lib.mops_mesh_create.restype = st
+    lib.mops_mesh_destroy.argtypes = [P]; lib.mops_mesh_destroy.restype = None
+    lib.mops_mesh_bytes.argtypes = [P]; lib.mops_mesh_bytes.restype = I64
+    lib.mops_field_create.argtypes = [P, P, P, P]; lib.mops_field_create.restype = st
+    lib.mops_field_create_derived.argtypes = [P, P, P, P, P, P]; lib.mops_field_create_derived.restype = st
+    lib.mops_field_export.argtypes = [P, P, P, P, P]; lib.mops_field_export.restype = st
+    lib.mops_cell_to_vertex_attr.argtypes = [P, P, P, P]; lib.mops_cell_to_vertex_attr.restype = st
+    lib.mops_field_destroy.argtypes = [P]; lib.mops_field_destroy.restype = None
+    lib.mops_field_bytes.argtypes = [P]; lib.mops_field_bytes.restype = I64
+    lib.mops_locate_cells.argtypes = [P, I64, P, P, P]; lib.mops_locate_cells.restype = st
+    lib.mops_traj_num_records.argtypes = [P]; lib.mops_traj_num_records.restype = I64
+    lib.mops_traj_num_steps.argtypes = [P]; lib.mops_traj_num_steps.restype = I64
+    lib.mops_traj_advance.argtypes = [P, P, P, P, P, I64, I64, P, I64, P]; lib.mops_traj_advance.restype = st
+    lib.mops_traj_finalize.argtypes = [I64, I64, P, P, I64, I32, P, P, P, P, P, P]
+    lib.mops_traj_finalize.restype = st
+    lib.mops_remove_nan_lines.argtypes = [I64, I64, P, P, P, P, P, P]; lib.mops_remove_nan_lines.restype = st
+    lib.mops_run_trajectories.argtypes = [P, P, P, P, I64, P, P, C.c_float, P, P, P, P, P, P, P, P, P, P]
+    lib.mops_run_trajectories.restype = st
+    _lib = lib
+    return lib
+
+
+def check(status: int, what: str = ""):
+    if status != MOPS_OK:
+        msg = load().mops_last_error().decode(errors="replace")
+        raise MopsError(f"{what} failed (status {status}): {msg}")

@@ -1,0 +1,1277 @@
+// mops_engine.hip -- MI355X (gfx950, CDNA4) particle-trajectory engine.
+//
+// Hand-written HIP for the reference's StreamLine / PathLine hot path
+// (YosefQiu/MOPS src/CPU/TBB/Kernel/MPASOVisualizerKernels.cpp:653-1496) and
+// its derived-field producers (src/CPU/TBB/MPASOSolutionTBB.cpp).  Written for
+// CDNA4 from the reference's semantics, not translated from its CUDA/HIP
+// backend:
+//
+//  * one lane per particle, wave64, all steps of a segment inside one launch;
+//    the particle state (position, float depth, cell) lives in registers and
+//    the per-cell stencil (vertex ids, vertex coordinates, neighbour ids and
+//    the polygon-only Wachspress terms B_i) is cached in registers across
+//    steps -- a particle keeps its cell for ~10^3 steps at dt = 120 s;
+//  * the mesh is re-laid out in HBM as one 64-B "cell record" per cell
+//    (nEdges, 0-based verticesOnCell, 0-based cellsOnCell) plus 32-B padded
+//    xyz rows, so every stencil fetch is whole sectors;
+//  * the zTop column is never materialised: a streaming pass applies the
+//    reference's monotone fix-up in order and derives the layer bracket from
+//    two monotone predicates, stopping at the first level below the particle
+//    (exactly the reference's result -- see bracket_scan);
+//  * FP64 throughout with -ffp-contract=off and the reference's operation
+//    order, so results are bit-comparable with the CPU path.
+//
+// No MFMA: this is a latency/bandwidth-bound gather.
+
+#include <hip/hip_runtime.h>
+#include <hipcub/hipcub.hpp>
+
+#include <algorithm>
+#include <cmath>
+#include <cstdint>
+#include <cstdio>
+#include <cstring>
+#include <limits>
+#include <string>
+#include <vector>
+
+#include "mops_traj.h"
+
+#define MOPS_ABI_VERSION 1
+
+namespace {
+
+thread_local std::string g_last_error;
+
+mops_status fail(mops_status st, const std::string& msg) {
+    g_last_error = msg;
+    return st;
+}
+
+#define HIP_TRY(expr)                                                                   \
+    do {                                                                                \
+        hipError_t _e = (expr);                                                         \
+        if (_e != hipSuccess)                                                           \
+            return fail(MOPS_ERR_HIP, std::string(#expr " failed: ") + hipGetErrorString(_e)); \
+    } while (0)
+
+constexpr int kMaxLevels = 100;  // reference MAX_VERTICAL_LEVEL_NUM
+constexpr int kMaxVertex = 20;   // reference MAX_VERTEX_NUM
+constexpr int kBlock = 256;
+
+inline int rec_ints_for(int maxv) { return ((1 + 2 * maxv) + 3) / 4 * 4; }
+
+}  // namespace
+
+struct mops_mesh {
+    int64_t C = 0, V = 0;
+    int maxE = 0, L = 0;
+    int maxv = 0;       // stencil capacity of the kernel instantiation (7, 12 or 20)
+    int rec_ints = 0;   // ints per cell record
+    int* d_cellrec = nullptr;    // [C][rec_ints]: nEdges | voc[maxv] | coc[maxv] (0-based, -1 none)
+    double4* d_cxyz = nullptr;   // [C] (x,y,z,0)
+    double4* d_vxyz = nullptr;   // [V]
+    int* d_cov = nullptr;        // [V][3] cellsOnVertex 0-based, -1 = missing (boundary)
+    // seed-location bucket index
+    double bucket_h = 0.0, bucket_origin = 0.0;
+    uint64_t* d_bkeys = nullptr;  // sorted bucket keys [C]
+    int* d_bcells = nullptr;      // cell ids in key order [C]
+    int64_t bytes = 0;
+};
+
+struct mops_field {
+    const mops_mesh* mesh = nullptr;
+    int64_t V = 0;
+    int L = 0;
+    double* d_zt = nullptr;   // cellVertexZTop [V][L]
+    double* d_vel = nullptr;  // cellVertexVelocity [V][L][3]
+    double* d_w = nullptr;    // cellVertexVertVelocity [V][L+1]
+    int64_t bytes = 0;
+};
+
+// ===========================================================================
+// device helpers -- every expression keeps the reference's evaluation order
+// ===========================================================================
+namespace dev {
+
+__device__ __forceinline__ double len3(double x, double y, double z) { return sqrt(x * x + y * y + z * z); }
+
+// Interpolator::triangle_area (Interpolation.hpp:95-110)
+__device__ __forceinline__ double tri_area(double ax, double ay, double az, double bx, double by, double bz,
+                                           double cx, double cy, double cz) {
+    const double e1x = bx - ax, e1y = by - ay, e1z = bz - az;
+    const double e2x = cx - ax, e2y = cy - ay, e2z = cz - az;
+    const double px = e1y * e2z - e1z * e2y;
+    const double py = e1z * e2x - e1x * e2z;
+    const double pz = e1x * e2y - e1y * e2x;
+    return sqrt(px * px + py * py + pz * pz) / 2.0;
+}
+
+// TBBKernel::CalcPositionAfterRotation (TBBKernel.h:177-206)
+__device__ __forceinline__ void rotate(double px, double py, double pz, double ax, double ay, double az, double th,
+                                       double& rx, double& ry, double& rz) {
+    const double c = cos(th), s = sin(th);
+    const double al = len3(ax, ay, az);
+    if (al <= 1e-12) { rx = px; ry = py; rz = pz; return; }
+    const double ux = ax / al, uy = ay / al, uz = az / al;
+    rx = (c + ux * ux * (1.0 - c)) * px + (ux * uy * (1.0 - c) - uz * s) * py + (ux * uz * (1.0 - c) + uy * s) * pz;
+    ry = (uy * ux * (1.0 - c) + uz * s) * px + (c + uy * uy * (1.0 - c)) * py + (uy * uz * (1.0 - c) - ux * s) * pz;
+    rz = (uz * ux * (1.0 - c) - uy * s) * px + (uz * uy * (1.0 - c) + ux * s) * py + (c + uz * uz * (1.0 - c)) * pz;
+}
+
+// advect_on_sphere lambda (MPASOVisualizerKernels.cpp:729-738)
+__device__ __forceinline__ void advect(double px, double py, double pz, double vx, double vy, double vz, double dt,
+                                       double& ox, double& oy, double& oz) {
+    const double rr = len3(px, py, pz), sp = len3(vx, vy, vz);
+    if (rr < 1e-12 || sp < 1e-12) { ox = px; oy = py; oz = pz; return; }
+    const double ax = py * vz - pz * vy, ay = pz * vx - px * vz, az = px * vy - py * vx;
+    const double th = (sp * dt) / rr;
+    rotate(px, py, pz, ax, ay, az, th, ox, oy, oz);
+}
+
+__device__ __forceinline__ double dmax(double a, double b) { return (a < b) ? b : a; }  // std::max
+__device__ __forceinline__ double dmin(double a, double b) { return (b < a) ? b : a; }  // std::min
+__device__ __forceinline__ double dclamp(double v, double lo, double hi) { return (v < lo) ? lo : (hi < v) ? hi : v; }
+
+// Per-cell stencil cached in registers while the particle stays in the cell.
+template <int MAXV>
+struct Cell {
+    int id;
+    int nv;
+    int vid[MAXV];
+    int coc[MAXV];
+    double x[MAXV], y[MAXV], z[MAXV];
+    double B[MAXV];  // Wachspress B_i = area(poly[i-1], poly[i], poly[i+1]) (depends on the polygon only)
+};
+
+template <int MAXV>
+__device__ __forceinline__ void load_cell(Cell<MAXV>& c, int cell, const int* __restrict__ cellrec,
+                                          const double4* __restrict__ vxyz) {
+    constexpr int REC = ((1 + 2 * MAXV) + 3) / 4 * 4;
+    const int* r = cellrec + (int64_t)cell * REC;
+    int buf[REC];
+#pragma unroll
+    for (int q = 0; q < REC / 4; ++q) {
+        const int4 v = reinterpret_cast<const int4*>(r)[q];
+        buf[4 * q] = v.x; buf[4 * q + 1] = v.y; buf[4 * q + 2] = v.z; buf[4 * q + 3] = v.w;
+    }
+    c.id = cell;
+    c.nv = buf[0];
+    const int nv = c.nv;
+#pragma unroll
+    for (int k = 0; k < MAXV; ++k) {
+        c.vid[k] = buf[1 + k];
+        c.coc[k] = buf[1 + MAXV + k];
+        if (k < nv) {
+            const double4 p = vxyz[c.vid[k]];
+            c.x[k] = p.x; c.y[k] = p.y; c.z[k] = p.z;
+        } else {
+            c.x[k] = 0.0; c.y[k] = 0.0; c.z[k] = 0.0;
+        }
+    }
+    double lx = 0, ly = 0, lz = 0;  // poly[nv-1]
+#pragma unroll
+    for (int k = 0; k < MAXV; ++k)
+        if (k == nv - 1) { lx = c.x[k]; ly = c.y[k]; lz = c.z[k]; }
+#pragma unroll
+    for (int i = 0; i < MAXV; ++i) {
+        if (i < nv) {
+            const double qx = (i == 0) ? lx : c.x[(i + MAXV - 1) % MAXV];
+            const double qy = (i == 0) ? ly : c.y[(i + MAXV - 1) % MAXV];
+            const double qz = (i == 0) ? lz : c.z[(i + MAXV - 1) % MAXV];
+            const bool wrap = (i + 1 >= nv);
+            const double nx = wrap ? c.x[0] : c.x[(i + 1) % MAXV];
+            const double ny = wrap ? c.y[0] : c.y[(i + 1) % MAXV];
+            const double nz = wrap ? c.z[0] : c.z[(i + 1) % MAXV];
+            c.B[i] = tri_area(qx, qy, qz, c.x[i], c.y[i], c.z[i], nx, ny, nz);
+        } else {
+            c.B[i] = 0.0;
+        }
+    }
+}
+
+// guards + TBBKernel::IsInMesh + Interpolator::CalcPolygonWachspress
+// (MPASOVisualizerKernels.cpp:744-770, TBBKernel.h:21-54, Interpolation.hpp:137-165)
+template <int MAXV>
+__device__ __forceinline__ bool weights(const Cell<MAXV>& c, int L, int V, double px, double py, double pz,
+                                        double* w) {
+    if (c.id < 0 || L <= 1 || L > kMaxLevels) return false;
+    const int nv = c.nv;
+    if (nv <= 0 || nv > kMaxVertex) return false;
+    if (!isfinite(px) || !isfinite(py) || !isfinite(pz)) return false;
+#pragma unroll
+    for (int k = 0; k < MAXV; ++k) {
+        if (k < nv) {
+            const bool wrap = (k + 1 >= nv);
+            const double bx = wrap ? c.x[0] : c.x[(k + 1) % MAXV];
+            const double by = wrap ? c.y[0] : c.y[(k + 1) % MAXV];
+            const double bz = wrap ? c.z[0] : c.z[(k + 1) % MAXV];
+            const double nx = c.y[k] * bz - c.z[k] * by;
+            const double ny = c.z[k] * bx - c.x[k] * bz;
+            const double nz = c.x[k] * by - c.y[k] * bx;
+            if (nx * px + ny * py + nz * pz < 0.0) return false;
+        }
+    }
+    // the reference validates vertex ids in the zTop loop (:776-779); no side
+    // effects happen before it, so checking up front is equivalent
+#pragma unroll
+    for (int k = 0; k < MAXV; ++k)
+        if (k < nv && (c.vid[k] < 0 || c.vid[k] >= V)) return false;
+    double lx = 0, ly = 0, lz = 0;
+#pragma unroll
+    for (int k = 0; k < MAXV; ++k)
+        if (k == nv - 1) { lx = c.x[k]; ly = c.y[k]; lz = c.z[k]; }
+    double sum = 0.0;
+    double Anext = tri_area(lx, ly, lz, c.x[0], c.y[0], c.z[0], px, py, pz);
+#pragma unroll
+    for (int i = 0; i < MAXV; ++i) {
+        if (i < nv) {
+            const double Ai = Anext;
+            const bool wrap = (i + 1 >= nv);
+            const double nx = wrap ? c.x[0] : c.x[(i + 1) % MAXV];
+            const double ny = wrap ? c.y[0] : c.y[(i + 1) % MAXV];
+            const double nz = wrap ? c.z[0] : c.z[(i + 1) % MAXV];
+            Anext = tri_area(c.x[i], c.y[i], c.z[i], nx, ny, nz, px, py, pz);
+            w[i] = c.B[i] / (Ai * Anext);
+            sum += w[i];
+        } else {
+            w[i] = 0.0;
+        }
+    }
+    const double recp = 1.0 / sum;
+#pragma unroll
+    for (int i = 0; i < MAXV; ++i)
+        if (i < nv) w[i] *= recp;
+    return true;
+}
+
+// one interpolated zTop level:  z = sum_v w_v * zTopV[v*L + k]  (v in order)
+template <int MAXV>
+__device__ __forceinline__ double col(const Cell<MAXV>& c, const double* w, const double* __restrict__ zt, int L,
+                                      int k) {
+    double acc = 0.0;
+#pragma unroll
+    for (int v = 0; v < MAXV; ++v)
+        if (v < c.nv) acc += w[v] * zt[(int64_t)c.vid[v] * L + k];
+    return acc;
+}
+
+// Layer bracket over the interpolated, monotone-fixed zTop column
+// (streamline :772-822, pathline :1156-1218) without materialising it.
+//
+// The fixed-up column z' (z'_k = z_k > z'_{k-1} ? z'_{k-1} - 1e-9 : z_k) is
+// non-increasing, so P(k) = d <= z'_{k-1}+eps is true exactly for k <= b and
+// Q(k) = d >= z'_k-eps exactly for k >= a (rounding is monotone).  Every
+// comparison the reference's binary search (streamline) or linear scan
+// (pathline) makes is P or Q, so its result is a function of (a, b) alone:
+// the scan stops at the first level where both are known.  If a exists the
+// reference's "below the bottom" test is provably false (z'_{L-1} <= z'_a).
+// Returns the layer (or -1 = fail) and z'_layer, z'_{layer-1}.
+template <int MAXV, bool PATH>
+__device__ __forceinline__ int bracket_scan(const Cell<MAXV>& c, const double* w, const double* __restrict__ zt,
+                                            int L, double d, double& zdn, double& zup) {
+    const double eps = 1e-8;
+    const double z0 = col<MAXV>(c, w, zt, L, 0);
+    double z1 = col<MAXV>(c, w, zt, L, 1);
+    if (z1 > z0) z1 = z0 - 1e-9;
+    if (d > z0 + eps) {  // above the surface (PATH: reference layer 0 reads z[-1])
+        zdn = z1; zup = z0;
+        return 1;
+    }
+    int a = -1, b = -1;
+    double za = 0, za_m1 = 0, zb = 0, zb_m1 = 0;
+    double zpp = z0, zp = z0;  // z'_{k-2}, z'_{k-1}
+    for (int k = 1; k < L; ++k) {
+        double zk;
+        if (k == 1) {
+            zk = z1;
+        } else {
+            zk = col<MAXV>(c, w, zt, L, k);
+            if (zk > zp) zk = zp - 1e-9;
+        }
+        const bool P = d <= zp + eps;
+        const bool Q = d >= zk - eps;
+        if (a < 0 && Q) { a = k; za = zk; za_m1 = zp; }
+        if (b < 0 && !P) { b = k - 1; zb = zp; zb_m1 = zpp; }
+        zpp = zp;
+        zp = zk;
+        if (a >= 0 && b >= 0) break;
+    }
+    if (b < 0) { b = L - 1; zb = zp; zb_m1 = zpp; }
+    if (a < 0) {  // scanned the whole column: zp = z'_{L-1}, zpp = z'_{L-2}
+        if (d < zp - eps) { zdn = zp; zup = zpp; return L - 1; }
+    }
+    int layer;
+    if (PATH) {
+        if (a < 0 || a > b) return -1;  // linear scan found nothing
+        layer = a;
+    } else {
+        const int aa = (a < 0) ? L : a;
+        int lo = 1, hi = L - 1, ans = 1;
+        while (lo <= hi) {
+            const int mid = (lo + hi) >> 1;
+            if (mid >= aa && mid <= b) { ans = mid; break; }
+            if (mid > b) hi = mid - 1; else lo = mid + 1;
+        }
+        layer = ans;
+    }
+    if (layer == a) { zdn = za; zup = za_m1; return layer; }
+    if (layer == b && b >= 2) { zdn = zb; zup = zb_m1; return layer; }
+    if (layer == 1) { zdn = z1; zup = z0; return 1; }
+    // rare (a level thinner than 2e-8 inside the bracket): recompute the chain
+    double p = z0, q = z0;
+    for (int k = 1; k <= layer; ++k) {
+        double zk = col<MAXV>(c, w, zt, L, k);
+        if (zk > p) zk = p - 1e-9;
+        q = p;
+        p = zk;
+    }
+    zdn = p; zup = q;
+    return layer;
+}
+
+template <int MAXV>
+__device__ __forceinline__ void vel_at(const Cell<MAXV>& c, const double* w, const double* __restrict__ vel, int L,
+                                       int layer, double& vx, double& vy, double& vz) {
+    vx = 0.0; vy = 0.0; vz = 0.0;
+#pragma unroll
+    for (int v = 0; v < MAXV; ++v) {
+        if (v < c.nv) {
+            const double* q = vel + ((int64_t)c.vid[v] * L + layer) * 3;
+            vx += w[v] * q[0];
+            vy += w[v] * q[1];
+            vz += w[v] * q[2];
+        }
+    }
+}
+
+template <int MAXV>
+__device__ __forceinline__ double attr_at(const Cell<MAXV>& c, const double* w, const double* __restrict__ a, int Lt,
+                                          int layer) {
+    double r = 0.0;
+#pragma unroll
+    for (int v = 0; v < MAXV; ++v)
+        if (v < c.nv) r += w[v] * a[(int64_t)c.vid[v] * Lt + layer];
+    return r;
+}
+
+struct Field {
+    const double* __restrict__ zt;
+    const double* __restrict__ vel;
+    const double* __restrict__ w;
+};
+
+// streamline calc_velocity_at (MPASOVisualizerKernels.cpp:740-872)
+template <int MAXV>
+__device__ __forceinline__ bool eval_stream(const Cell<MAXV>& c, int L, int V, const Field& f, double px, double py,
+                                            double pz, double d, double& hx, double& hy, double& hz, double& wv) {
+    double w[MAXV];
+    if (!weights<MAXV>(c, L, V, px, py, pz, w)) return false;
+    double zdn, zup;
+    const int layer = bracket_scan<MAXV, false>(c, w, f.zt, L, d, zdn, zup);
+    if (layer < 0) return false;
+    double x = d;
+    x = dmax(zdn, dmin(x, zup));
+    const double den = zup - zdn;
+    if (fabs(den) < 1e-12) return false;
+    const double t = (x - zdn) / den;
+    double dx, dy, dz, ux, uy, uz;
+    vel_at<MAXV>(c, w, f.vel, L, layer, dx, dy, dz);
+    vel_at<MAXV>(c, w, f.vel, L, layer - 1, ux, uy, uz);
+    if (len3(dx, dy, dz) < 1e-12 || len3(ux, uy, uz) < 1e-12) return false;
+    hx = ux * t + dx * (1.0 - t);
+    hy = uy * t + dy * (1.0 - t);
+    hz = uz * t + dz * (1.0 - t);
+    if (len3(hx, hy, hz) < 1e-12) return false;
+    const int Lp1 = L + 1;
+    int dn_if = layer, up_if = (layer > 0) ? (layer - 1) : 0;
+    if (dn_if >= Lp1) dn_if = Lp1 - 1;
+    if (up_if >= Lp1) up_if = Lp1 - 1;
+    const double wdn = attr_at<MAXV>(c, w, f.w, Lp1, dn_if);
+    const double wup = attr_at<MAXV>(c, w, f.w, Lp1, up_if);
+    wv = t * wup + (1.0 - t) * wdn;
+    return true;
+}
+
+// pathline calc_velocity_at (MPASOVisualizerKernels.cpp:1124-1327).  The
+// attribute channel is not evaluated: FinalizeTrajectoryLinesWithAttrs never
+// reads it (TrajectoryCommon.h:176-185, quirk Q9), so it is unobservable.
+template <int MAXV>
+__device__ __forceinline__ bool eval_path(const Cell<MAXV>& c, int L, int V, const Field& ff, const Field& fb,
+                                          double px, double py, double pz, double d, double alpha, double& hx,
+                                          double& hy, double& hz, double& wv) {
+    double w[MAXV];
+    if (!weights<MAXV>(c, L, V, px, py, pz, w)) return false;
+    double zfdn, zfup, zbdn, zbup;
+    const int lf = bracket_scan<MAXV, true>(c, w, ff.zt, L, d, zfdn, zfup);
+    const int lb = bracket_scan<MAXV, true>(c, w, fb.zt, L, d, zbdn, zbup);
+    if (lf < 0 || lb < 0) return false;
+    const double xf = dmax(zfdn, dmin(d, zfup));
+    const double denf = zfup - zfdn;
+    if (fabs(denf) < 1e-12) return false;
+    const double tf = (xf - zfdn) / denf;
+    const double xb = dmax(zbdn, dmin(d, zbup));
+    const double denb = zbup - zbdn;
+    if (fabs(denb) < 1e-12) return false;
+    const double tb = (xb - zbdn) / denb;
+    double ax, ay, az, bx, by, bz;
+    vel_at<MAXV>(c, w, ff.vel, L, lf, ax, ay, az);
+    vel_at<MAXV>(c, w, ff.vel, L, lf - 1, bx, by, bz);
+    const double fx = bx * tf + ax * (1.0 - tf), fy = by * tf + ay * (1.0 - tf), fz = bz * tf + az * (1.0 - tf);
+    vel_at<MAXV>(c, w, fb.vel, L, lb, ax, ay, az);
+    vel_at<MAXV>(c, w, fb.vel, L, lb - 1, bx, by, bz);
+    const double gx = bx * tb + ax * (1.0 - tb), gy = by * tb + ay * (1.0 - tb), gz = bz * tb + az * (1.0 - tb);
+    hx = gx * alpha + fx * (1.0 - alpha);
+    hy = gy * alpha + fy * (1.0 - alpha);
+    hz = gz * alpha + fz * (1.0 - alpha);
+    const int Lp1 = L + 1;
+    int dnf = lf, upf = (lf > 0) ? lf - 1 : 0, dnb = lb, upb = (lb > 0) ? lb - 1 : 0;
+    if (dnf >= Lp1) dnf = Lp1 - 1;
+    if (upf >= Lp1) upf = Lp1 - 1;
+    if (dnb >= Lp1) dnb = Lp1 - 1;
+    if (upb >= Lp1) upb = Lp1 - 1;
+    const double wdnf = attr_at<MAXV>(c, w, ff.w, Lp1, dnf), wupf = attr_at<MAXV>(c, w, ff.w, Lp1, upf);
+    const double wf = tf * wupf + (1.0 - tf) * wdnf;
+    const double wdnb = attr_at<MAXV>(c, w, fb.w, Lp1, dnb), wupb = attr_at<MAXV>(c, w, fb.w, Lp1, upb);
+    const double wb = tb * wupb + (1.0 - tb) * wdnb;
+    wv = alpha * wb + (1.0 - alpha) * wf;
+    return true;
+}
+
+}  // namespace dev
+
+// ===========================================================================
+// trajectory kernel
+// ===========================================================================
+struct TrajArgs {
+    const int* __restrict__ cellrec;
+    const double4* __restrict__ cxyz;
+    const double4* __restrict__ vxyz;
+    int C, V, L;
+    dev::Field f0, f1;
+    double* px; double* py; double* pz;
+    float* depth;
+    int* cell;
+    int* death;
+    int64_t n;
+    int64_t step_begin, step_end, n_steps;
+    int delta_t;          // signed (dt_sign * deltaT)
+    double dalpha;        // pathline RK4: dt / simulationDuration
+    int64_t rec_period;   // record at step j iff (j+1) % rec_period == 0 (0 = never)
+    int64_t K;
+    double* rec;
+    int64_t rec_stride;
+};
+
+template <int MAXV, bool PATH, bool EULER>
+__global__ void __launch_bounds__(kBlock) traj_kernel(TrajArgs a) {
+    const int64_t pid = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (pid >= a.n) return;
+    if (a.death[pid] >= 0) return;  // the reference's lambda has returned
+    double x = a.px[pid], y = a.py[pid], z = a.pz[pid];
+    float dep = a.depth[pid];
+    int cell = a.cell[pid];
+    int died = -1;
+    dev::Cell<MAXV> c;
+    c.id = -1;
+    c.nv = 0;
+    const int C = a.C;
+    for (int64_t step = a.step_begin; step < a.step_end; ++step) {
+        if (step == 0) {  // first_loop (:892-901)
+            if (cell < 0 || cell >= C) { died = 0; break; }
+            dev::load_cell<MAXV>(c, cell, a.cellrec, a.vxyz);
+            double* r0 = a.rec;
+            r0[0 * a.rec_stride + pid] = x;
+            r0[1 * a.rec_stride + pid] = y;
+            r0[2 * a.rec_stride + pid] = z;
+        } else {  // one-hop nearest-centre walk (:902-922)
+            if (cell < 0 || cell >= C) { died = (int)step; break; }
+            if (c.id != cell) dev::load_cell<MAXV>(c, cell, a.cellrec, a.vxyz);
+            double best = 1.7976931348623157e308;
+            int nc = cell;
+#pragma unroll
+            for (int n = 0; n <= MAXV; ++n) {
+                if (n <= c.nv) {
+                    int cid;
+                    if (n < MAXV) cid = (n < c.nv) ? c.coc[n] : cell; else cid = cell;
+                    if (cid >= 0 && cid < C) {
+                        const double4 q = a.cxyz[cid];
+                        const double l = dev::len3(q.x - x, q.y - y, q.z - z);
+                        if (l < best) { best = l; nc = cid; }
+                    }
+                }
+            }
+            cell = nc;
+            if (c.id != cell) dev::load_cell<MAXV>(c, cell, a.cellrec, a.vxyz);
+        }
+        const double d = -1.0 * (double)dep;
+        const double r = dev::len3(x, y, z);
+        double hx = 0, hy = 0, hz = 0, wv = 0;
+        double nx, ny, nz;
+        const double alpha = PATH ? (double)step / (double)a.n_steps : 0.0;
+        if (EULER) {
+            bool ok = PATH ? dev::eval_path<MAXV>(c, a.L, a.V, a.f0, a.f1, x, y, z, d, alpha, hx, hy, hz, wv)
+                           : dev::eval_stream<MAXV>(c, a.L, a.V, a.f0, x, y, z, d, hx, hy, hz, wv);
+            if (!ok) { died = (int)step; break; }
+            const double ax = y * hz - z * hy, ay = z * hx - x * hz, az = x * hy - y * hx;
+            const double speed = dev::len3(hx, hy, hz);
+            const double th = (speed * a.delta_t) / dev::dmax(1e-12, r);
+            dev::rotate(x, y, z, ax, ay, az, th, nx, ny, nz);
+        } else {
+            const double dt = (double)a.delta_t;
+            double s1x, s1y, s1z, s1w, s2x, s2y, s2z, s2w, s3x, s3y, s3z, s3w, s4x, s4y, s4z, s4w;
+            double qx, qy, qz;
+            const double a1 = alpha;
+            bool ok = PATH ? dev::eval_path<MAXV>(c, a.L, a.V, a.f0, a.f1, x, y, z, d, a1, s1x, s1y, s1z, s1w)
+                           : dev::eval_stream<MAXV>(c, a.L, a.V, a.f0, x, y, z, d, s1x, s1y, s1z, s1w);
+            if (!ok) { died = (int)step; break; }
+            dev::advect(x, y, z, s1x, s1y, s1z, dt * 0.5, qx, qy, qz);
+            const double a2 = PATH ? dev::dclamp(a1 + 0.5 * a.dalpha, 0.0, 1.0) : 0.0;
+            ok = PATH ? dev::eval_path<MAXV>(c, a.L, a.V, a.f0, a.f1, qx, qy, qz, d, a2, s2x, s2y, s2z, s2w)
+                      : dev::eval_stream<MAXV>(c, a.L, a.V, a.f0, qx, qy, qz, d, s2x, s2y, s2z, s2w);
+            if (!ok) { died = (int)step; break; }
+            dev::advect(x, y, z, s2x, s2y, s2z, dt * 0.5, qx, qy, qz);
+            ok = PATH ? dev::eval_path<MAXV>(c, a.L, a.V, a.f0, a.f1, qx, qy, qz, d, a2, s3x, s3y, s3z, s3w)
+                      : dev::eval_stream<MAXV>(c, a.L, a.V, a.f0, qx, qy, qz, d, s3x, s3y, s3z, s3w);
+            if (!ok) { died = (int)step; break; }
+            dev::advect(x, y, z, s3x, s3y, s3z, dt, qx, qy, qz);
+            const double a4 = PATH ? dev::dclamp(a1 + a.dalpha, 0.0, 1.0) : 0.0;
+            ok = PATH ? dev::eval_path<MAXV>(c, a.L, a.V, a.f0, a.f1, qx, qy, qz, d, a4, s4x, s4y, s4z, s4w)
+                      : dev::eval_stream<MAXV>(c, a.L, a.V, a.f0, qx, qy, qz, d, s4x, s4y, s4z, s4w);
+            if (!ok) { died = (int)step; break; }
+            // (s1 + 2 s2 + 2 s3 + s4) / 6 -- cy::Vec3 operator order (:959-960)
+            hx = (((s1x + s2x * 2.0) + s3x * 2.0) + s4x) / 6.0;
+            hy = (((s1y + s2y * 2.0) + s3y * 2.0) + s4y) / 6.0;
+            hz = (((s1z + s2z * 2.0) + s3z * 2.0) + s4z) / 6.0;
+            wv = (s1w + 2.0 * s2w + 2.0 * s3w + s4w) / 6.0;
+            const double tx = x + hx * dt, ty = y + hy * dt, tz = z + hz * dt;
+            const double tl = dev::len3(tx, ty, tz);
+            if (tl > 1e-12) { nx = (tx / tl) * r; ny = (ty / tl) * r; nz = (tz / tl) * r; }
+            else { nx = x; ny = y; nz = z; }
+        }
+        // vertical update (:977-986)
+        const double old_depth = (double)dep;
+        double nd = old_depth - wv * (double)a.delta_t;
+        nd = dev::dmax(0.0, nd);
+        const double r_new = dev::dmax(1.0, r + wv * (double)a.delta_t);
+        dep = (float)nd;
+        const double nl = dev::len3(nx, ny, nz);
+        if (nl > 1e-12) { nx = (nx / nl) * r_new; ny = (ny / nl) * r_new; nz = (nz / nl) * r_new; }
+        if (step == 0) {  // first_vel (:988-991)
+            a.rec[3 * a.rec_stride + pid] = hx;
+            a.rec[4 * a.rec_stride + pid] = hy;
+            a.rec[5 * a.rec_stride + pid] = hz;
+        }
+        x = nx; y = ny; z = nz;
+        if (a.rec_period > 0 && ((step + 1) % a.rec_period) == 0) {
+            const int64_t k = (step + 1) / a.rec_period - 1;
+            if (k < a.K) {
+                double* rk = a.rec + k * 6 * a.rec_stride;
+                rk[0 * a.rec_stride + pid] = x;
+                rk[1 * a.rec_stride + pid] = y;
+                rk[2 * a.rec_stride + pid] = z;
+                rk[3 * a.rec_stride + pid] = hx;
+                rk[4 * a.rec_stride + pid] = hy;
+                rk[5 * a.rec_stride + pid] = hz;
+            }
+        }
+    }
+    a.px[pid] = x; a.py[pid] = y; a.pz[pid] = z;
+    a.depth[pid] = dep;
+    a.cell[pid] = cell;
+    if (died >= 0) a.death[pid] = died;
+}
+
+// ===========================================================================
+// output assembly: FinalizeTrajectoryLines[WithAttrs] + RemoveNaN
+// ===========================================================================
+__device__ __forceinline__ bool finite3(double a, double b, double c) { return isfinite(a) && isfinite(b) && isfinite(c); }
+
+__global__ void remove_nan_kernel(int64_t n, int64_t P, double* pts, double* vel, double* tmp, double* sal,
+                                  double* last) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    double* pp = pts + 3 * i * P;
+    double* vv = vel ? vel + 3 * i * P : nullptr;
+    double* tt = tmp ? tmp + i * P : nullptr;
+    double* ss = sal ? sal + i * P : nullptr;
+    int64_t k = 0;
+    for (; k < P; ++k)
+        if (!finite3(pp[3 * k], pp[3 * k + 1], pp[3 * k + 2])) break;
+    if (k < P) {
+        const int64_t src = (k == 0) ? 0 : k - 1;
+        const double lx = pp[3 * src], ly = pp[3 * src + 1], lz = pp[3 * src + 2];
+        const double lt = tt ? tt[src] : 0.0, ls = ss ? ss[src] : 0.0;
+        const int64_t j0 = (k == 0) ? 0 : k - 1;
+        for (int64_t j = j0; j < P; ++j) {
+            if (j >= k || k == 0) {
+                pp[3 * j] = lx; pp[3 * j + 1] = ly; pp[3 * j + 2] = lz;
+                if (tt) tt[j] = lt;
+                if (ss) ss[j] = ls;
+            }
+            if (vv) { vv[3 * j] = 0.0; vv[3 * j + 1] = 0.0; vv[3 * j + 2] = 0.0; }
+        }
+    }
+    if (last) {
+        last[3 * i] = pp[3 * (P - 1)];
+        last[3 * i + 1] = pp[3 * (P - 1) + 1];
+        last[3 * i + 2] = pp[3 * (P - 1) + 2];
+    }
+}
+
+__global__ void assemble_kernel(int64_t n, int64_t K, const double* seeds, const double* rec, int64_t stride,
+                                int pathline, double* pts, double* vel, double* tmp, double* sal) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const int64_t P = K + 1;
+    double* pp = pts + 3 * i * P;
+    pp[0] = seeds[3 * i]; pp[1] = seeds[3 * i + 1]; pp[2] = seeds[3 * i + 2];
+    for (int64_t k = 0; k < K; ++k) {
+        const double* rk = rec + k * 6 * stride;
+        pp[3 * (k + 1)] = rk[i];
+        pp[3 * (k + 1) + 1] = rk[stride + i];
+        pp[3 * (k + 1) + 2] = rk[2 * stride + i];
+        if (vel) {
+            vel[3 * (i * P + k)] = rk[3 * stride + i];
+            vel[3 * (i * P + k) + 1] = rk[4 * stride + i];
+            vel[3 * (i * P + k) + 2] = rk[5 * stride + i];
+        }
+        if (tmp) tmp[i * P + k] = pathline ? rk[3 * stride + i] : 0.0;
+        if (sal) sal[i * P + k] = pathline ? rk[4 * stride + i] : 0.0;
+    }
+    if (vel) { vel[3 * (i * P + K)] = 0.0; vel[3 * (i * P + K) + 1] = 0.0; vel[3 * (i * P + K) + 2] = 0.0; }
+    if (tmp) tmp[i * P + K] = 0.0;
+    if (sal) sal[i * P + K] = 0.0;
+}
+
+// ===========================================================================
+// derived-field preprocessing (once per snapshot)
+// ===========================================================================
+
+// MPASOSolution::calcCellCenterZtop (MPASOSolution.cpp:535-618)
+__global__ void cell_ztop_kernel(int64_t C, int L, const double* thick, const double* bottom, const double* ssh,
+                                 double* ztop) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= C) return;
+    if (bottom) {
+        double z = -bottom[i];
+        for (int k = L - 1; k >= 0; --k) { z += thick[L * i + k]; ztop[i * L + k] = z * 1.0; }
+    } else if (ssh) {
+        double z = ssh[i];
+        ztop[i * L] = z * 1.0;
+        for (int j = 1; j < L; ++j) { z -= thick[L * i + j - 1]; ztop[i * L + j] = z * 1.0; }
+    } else {
+        double prev = 0.0;
+        ztop[i * L] = 0.0;
+        for (int j = 1; j < L; ++j) { prev = prev - thick[L * i + j - 1]; ztop[i * L + j] = prev * 1.0; }
+    }
+}
+
+// CalcCellCenterVelocityByZM + GeoConverter::convertENUVelocityToXYZ (Uup = 0)
+__global__ void center_vel_zm_kernel(int64_t C, int L, const double4* cxyz, const double* zonal, const double* mer,
+                                     double* out) {
+    const int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (idx >= C * L) return;
+    const int64_t c = idx / L;
+    const double4 p = cxyz[c];
+    const double uz = zonal[idx], um = mer[idx], uu = 0.0;
+    double* o = out + 3 * idx;
+    if (p.x == 0.0 && p.y == 0.0) { o[0] = 0.0; o[1] = 0.0; o[2] = uu; return; }
+    const double Rxy = sqrt(p.x * p.x + p.y * p.y);
+    const double Rxyz = sqrt(p.x * p.x + p.y * p.y + p.z * p.z);
+    const double slon = p.y / Rxy, clon = p.x / Rxy, slat = p.z / Rxyz, clat = Rxy / Rxyz;
+    o[0] = -slon * uz - slat * clon * um + clon * clat * uu;
+    o[1] = clon * uz - slat * slon * um + slon * clat * uu;
+    o[2] = clat * um + slat * uu;
+}
+
+// CalcCellVertexZtop / CenterToVertex / VertexVelocity / VertexVertVelocity
+// (MPASOSolutionTBB.cpp:9-106, 270-366): barycentric of the 3 cellsOnVertex.
+template <int DIM>
+__global__ void cell_to_vertex_kernel(int64_t V, int Lt, const int* cov, const double4* cxyz, const double4* vxyz,
+                                      const double* src, double* dst, int clamp_neg) {
+    const int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (idx >= V * Lt) return;
+    const int64_t vid = idx / Lt;
+    const int k = (int)(idx % Lt);
+    const int c0 = cov[3 * vid], c1 = cov[3 * vid + 1], c2 = cov[3 * vid + 2];
+    double out[DIM];
+#pragma unroll
+    for (int d = 0; d < DIM; ++d) out[d] = 0.0;
+    if (c0 >= 0 && c1 >= 0 && c2 >= 0) {
+        const double4 p = vxyz[vid], A = cxyz[c0], B = cxyz[c1], Cc = cxyz[c2];
+        const double v0x = B.x - A.x, v0y = B.y - A.y, v0z = B.z - A.z;
+        const double v1x = Cc.x - A.x, v1y = Cc.y - A.y, v1z = Cc.z - A.z;
+        const double v2x = p.x - A.x, v2y = p.y - A.y, v2z = p.z - A.z;
+        const double d00 = v0x * v0x + v0y * v0y + v0z * v0z;
+        const double d01 = v0x * v1x + v0y * v1y + v0z * v1z;
+        const double d11 = v1x * v1x + v1y * v1y + v1z * v1z;
+        const double d20 = v2x * v0x + v2y * v0y + v2z * v0z;
+        const double d21 = v2x * v1x + v2y * v1y + v2z * v1z;
+        const double den = d00 * d11 - d01 * d01;
+        const double v = (d11 * d20 - d01 * d21) / den;
+        const double w = (d00 * d21 - d01 * d20) / den;
+        const double u = 1.0 - v - w;
+#pragma unroll
+        for (int d = 0; d < DIM; ++d) {
+            const double a0 = src[((int64_t)c0 * Lt + k) * DIM + d];
+            const double a1 = src[((int64_t)c1 * Lt + k) * DIM + d];
+            const double a2 = src[((int64_t)c2 * Lt + k) * DIM + d];
+            double o = u * a0 + v * a1 + w * a2;
+            if (clamp_neg && o < 0.0) o = 0.0;
+            out[d] = o;
+        }
+    }
+#pragma unroll
+    for (int d = 0; d < DIM; ++d) dst[idx * DIM + d] = out[d];
+}
+
+// ===========================================================================
+// seed location: exact 1-NN through a uniform 3-D bucket grid
+// ===========================================================================
+__device__ __forceinline__ uint64_t bkey(int64_t ix, int64_t iy, int64_t iz) {
+    return ((uint64_t)ix << 42) | ((uint64_t)iy << 21) | (uint64_t)iz;
+}
+
+__global__ void bucket_keys_kernel(int64_t C, const double4* cxyz, double origin, double h, uint64_t* keys,
+                                   int* ids) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= C) return;
+    const double4 p = cxyz[i];
+    const int64_t ix = (int64_t)floor((p.x - origin) / h), iy = (int64_t)floor((p.y - origin) / h),
+                  iz = (int64_t)floor((p.z - origin) / h);
+    keys[i] = bkey(ix, iy, iz);
+    ids[i] = (int)i;
+}
+
+__device__ __forceinline__ int64_t lower_bound_u64(const uint64_t* a, int64_t n, uint64_t key) {
+    int64_t lo = 0, hi = n;
+    while (lo < hi) {
+        const int64_t mid = (lo + hi) >> 1;
+        if (a[mid] < key) lo = mid + 1; else hi = mid;
+    }
+    return lo;
+}
+
+__device__ __forceinline__ void consider(const double4* cxyz, int cid, double qx, double qy, double qz, double& best,
+                                         int& bi) {
+    const double4 p = cxyz[cid];
+    const double d0 = qx - p.x, d1 = qy - p.y, d2 = qz - p.z;
+    double dd = 0.0;
+    dd += d0 * d0; dd += d1 * d1; dd += d2 * d2;
+    if (dd < best || (dd == best && cid < bi)) { best = dd; bi = cid; }
+}
+
+__global__ void locate_kernel(int64_t n, const double* pts, int64_t C, const double4* cxyz, const uint64_t* keys,
+                              const int* ids, double origin, double h, int* out) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const double qx = pts[3 * i], qy = pts[3 * i + 1], qz = pts[3 * i + 2];
+    double best = INFINITY;
+    int bi = -1;
+    const int kMaxShell = 6;
+    const int64_t kLim = (int64_t)1 << 21;
+    bool done = false;
+    if (isfinite(qx) && isfinite(qy) && isfinite(qz)) {
+        const int64_t bx = (int64_t)floor((qx - origin) / h), by = (int64_t)floor((qy - origin) / h),
+                      bz = (int64_t)floor((qz - origin) / h);
+        for (int s = 0; s <= kMaxShell && !done; ++s) {
+            for (int dx = -s; dx <= s; ++dx)
+                for (int dy = -s; dy <= s; ++dy)
+                    for (int dz = -s; dz <= s; ++dz) {
+                        const int m = max(abs(dx), max(abs(dy), abs(dz)));
+                        if (m != s) continue;
+                        const int64_t ix = bx + dx, iy = by + dy, iz = bz + dz;
+                        if (ix < 0 || iy < 0 || iz < 0 || ix >= kLim || iy >= kLim || iz >= kLim) continue;
+                        const uint64_t key = bkey(ix, iy, iz);
+                        int64_t j = lower_bound_u64(keys, C, key);
+                        for (; j < C && keys[j] == key; ++j) consider(cxyz, ids[j], qx, qy, qz, best, bi);
+                    }
+            // every point outside shells 0..s is at least s*h away
+            const double bound = (double)s * h;
+            if (bi >= 0 && best <= bound * bound) done = true;
+        }
+        if (!done) {  // far from every cell centre: exhaustive scan
+            for (int64_t cid = 0; cid < C; ++cid) consider(cxyz, (int)cid, qx, qy, qz, best, bi);
+        }
+    }
+    out[i] = bi;
+}
+
+// ===========================================================================
+// host side
+// ===========================================================================
+namespace {
+
+template <typename T>
+mops_status dmalloc(T** p, size_t count, int64_t* acc) {
+    if (count == 0) count = 1;
+    hipError_t e = hipMalloc(reinterpret_cast<void**>(p), count * sizeof(T));
+    if (e != hipSuccess) return fail(MOPS_ERR_HIP, std::string("hipMalloc failed: ") + hipGetErrorString(e));
+    if (acc) *acc += (int64_t)(count * sizeof(T));
+    return MOPS_OK;
+}
+
+#define MOPS_TRY(expr)                 \
+    do {                               \
+        mops_status _s = (expr);       \
+        if (_s != MOPS_OK) return _s;  \
+    } while (0)
+
+inline unsigned grid_for(int64_t n) { return (unsigned)((n + kBlock - 1) / kBlock); }
+
+int pick_maxv(int maxE) {
+    if (maxE <= 7) return 7;
+    if (maxE <= 12) return 12;
+    return 20;
+}
+
+mops_status upload_xyz(const double* h, int64_t n, double4** d, int64_t* acc, hipStream_t s) {
+    std::vector<double4> tmp((size_t)n);
+    for (int64_t i = 0; i < n; ++i) tmp[i] = make_double4(h[3 * i], h[3 * i + 1], h[3 * i + 2], 0.0);
+    MOPS_TRY(dmalloc(d, (size_t)n, acc));
+    HIP_TRY(hipMemcpyAsync(*d, tmp.data(), n * sizeof(double4), hipMemcpyHostToDevice, s));
+    HIP_TRY(hipStreamSynchronize(s));
+    return MOPS_OK;
+}
+
+template <typename T>
+mops_status upload(const T* h, size_t count, T** d, int64_t* acc, hipStream_t s) {
+    MOPS_TRY(dmalloc(d, count, acc));
+    HIP_TRY(hipMemcpyAsync(*d, h, count * sizeof(T), hipMemcpyHostToDevice, s));
+    return MOPS_OK;
+}
+
+void free_mesh(mops_mesh* m) {
+    if (!m) return;
+    (void)hipFree(m->d_cellrec); (void)hipFree(m->d_cxyz); (void)hipFree(m->d_vxyz); (void)hipFree(m->d_cov);
+    (void)hipFree(m->d_bkeys); (void)hipFree(m->d_bcells);
+    delete m;
+}
+
+void free_field(mops_field* f) {
+    if (!f) return;
+    (void)hipFree(f->d_zt); (void)hipFree(f->d_vel); (void)hipFree(f->d_w);
+    delete f;
+}
+
+}  // namespace
+
+int64_t gcd64(int64_t a, int64_t b) {
+    while (b) { int64_t t = a % b; a = b; b = t; }
+    return a;
+}
+
+template <int MAXV>
+void launch_traj(const TrajArgs& a, bool path, bool euler, hipStream_t s) {
+    const unsigned g = grid_for(a.n);
+    if (path) {
+        if (euler) traj_kernel<MAXV, true, true><<<g, kBlock, 0, s>>>(a);
+        else traj_kernel<MAXV, true, false><<<g, kBlock, 0, s>>>(a);
+    } else {
+        if (euler) traj_kernel<MAXV, false, true><<<g, kBlock, 0, s>>>(a);
+        else traj_kernel<MAXV, false, false><<<g, kBlock, 0, s>>>(a);
+    }
+}
+
+extern "C" {
+
+const char* mops_last_error(void) { return g_last_error.c_str(); }
+int32_t mops_abi_version(void) { return MOPS_ABI_VERSION; }
+
+mops_status mops_mesh_create(const mops_mesh_desc* desc, void* stream, mops_mesh** out) {
+    if (!desc || !out) return fail(MOPS_ERR_INVALID, "mops_mesh_create: null argument");
+    *out = nullptr;
+    const int64_t C = desc->n_cells, V = desc->n_vertices;
+    const int maxE = desc->max_edges, L = desc->n_vert_levels;
+    if (C <= 0 || V <= 0 || maxE <= 0 || L <= 0 || C >= INT32_MAX || V >= INT32_MAX)
+        return fail(MOPS_ERR_INVALID, "mops_mesh_create: invalid sizes");
+    if (maxE > kMaxVertex)
+        return fail(MOPS_ERR_UNSUPPORTED, "mops_mesh_create: maxEdges > 20 (reference MAX_VERTEX_NUM)");
+    if (!desc->h_n_edges_on_cell || !desc->h_vertices_on_cell || !desc->h_cells_on_cell || !desc->h_cell_coord ||
+        !desc->h_vertex_coord)
+        return fail(MOPS_ERR_INVALID, "mops_mesh_create: missing mesh array");
+    hipStream_t s = (hipStream_t)stream;
+    mops_mesh* m = new mops_mesh();
+    m->C = C; m->V = V; m->maxE = maxE; m->L = L;
+    m->maxv = pick_maxv(maxE);
+    m->rec_ints = rec_ints_for(m->maxv);
+    // ---- cell records (validated) ----
+    std::vector<int> rec((size_t)C * m->rec_ints, -1);
+    for (int64_t c = 0; c < C; ++c) {
+        const uint64_t ne = desc->h_n_edges_on_cell[c];
+        if (ne > (uint64_t)maxE) { free_mesh(m); return fail(MOPS_ERR_INVALID, "nEdgesOnCell > maxEdges"); }
+        int* r = rec.data() + c * m->rec_ints;
+        r[0] = (int)ne;
+        for (int k = 0; k < maxE; ++k) {
+            const uint64_t v1 = desc->h_vertices_on_cell[c * maxE + k];
+            const uint64_t c1 = desc->h_cells_on_cell[c * maxE + k];
+            if (k < (int)ne) {
+                if (v1 < 1 || v1 > (uint64_t)V) {
+                    free_mesh(m);
+                    return fail(MOPS_ERR_INVALID, "verticesOnCell entry out of range for an active edge");
+                }
+                r[1 + k] = (int)(v1 - 1);
+            }
+            // walk candidates: the reference skips cid < 0 || cid >= C (:910)
+            r[1 + m->maxv + k] = (c1 >= 1 && c1 <= (uint64_t)C) ? (int)(c1 - 1) : -1;
+        }
+    }
+    int64_t acc = 0;
+    mops_status st;
+    if ((st = upload(rec.data(), rec.size(), &m->d_cellrec, &acc, s)) != MOPS_OK) { free_mesh(m); return st; }
+    if ((st = upload_xyz(desc->h_cell_coord, C, &m->d_cxyz, &acc, s)) != MOPS_OK) { free_mesh(m); return st; }
+    if ((st = upload_xyz(desc->h_vertex_coord, V, &m->d_vxyz, &acc, s)) != MOPS_OK) { free_mesh(m); return st; }
+    if (desc->h_cells_on_vertex) {
+        std::vector<int> cov((size_t)V * 3);
+        for (int64_t i = 0; i < V * 3; ++i) {
+            const uint64_t x = desc->h_cells_on_vertex[i];
+            // reference boundary test: (x - 1) > C + 1 as size_t (Q10); ids C, C+1
+            // would read out of range there -- rejected here
+            if (x == 0 || x - 1 > (uint64_t)(C + 1)) cov[i] = -1;
+            else if (x - 1 >= (uint64_t)C) {
+                free_mesh(m);
+                return fail(MOPS_ERR_INVALID, "cellsOnVertex entry in [C+1, C+2] (reference reads out of range)");
+            } else cov[i] = (int)(x - 1);
+        }
+        if ((st = upload(cov.data(), cov.size(), &m->d_cov, &acc, s)) != MOPS_OK) { free_mesh(m); return st; }
+    }
+    // ---- bucket index for seed location ----
+    double rmax = 0.0, rsum = 0.0;
+    for (int64_t c = 0; c < C; ++c) {
+        const double* p = desc->h_cell_coord + 3 * c;
+        const double r = std::sqrt(p[0] * p[0] + p[1] * p[1] + p[2] * p[2]);
+        rmax = std::max(rmax, r);
+        rsum += r;
+    }
+    const double rmean = rsum / (double)C;
+    const double spacing = std::sqrt(4.0 * M_PI * rmean * rmean / (double)C);
+    m->bucket_h = std::max(2.0 * spacing, 1e-9);
+    m->bucket_origin = -(rmax * 1.05 + 4.0 * m->bucket_h);
+    if ((2.0 * -m->bucket_origin) / m->bucket_h >= (double)((int64_t)1 << 21)) {
+        free_mesh(m);
+        return fail(MOPS_ERR_UNSUPPORTED, "mesh too fine for the 21-bit bucket grid");
+    }
+    uint64_t *keys_in = nullptr;
+    int* ids_in = nullptr;
+    if ((st = dmalloc(&keys_in, (size_t)C, nullptr)) != MOPS_OK) { free_mesh(m); return st; }
+    if ((st = dmalloc(&ids_in, (size_t)C, nullptr)) != MOPS_OK) { (void)hipFree(keys_in); free_mesh(m); return st; }
+    if ((st = dmalloc(&m->d_bkeys, (size_t)C, &acc)) != MOPS_OK ||
+        (st = dmalloc(&m->d_bcells, (size_t)C, &acc)) != MOPS_OK) {
+        (void)hipFree(keys_in); (void)hipFree(ids_in); free_mesh(m); return st;
+    }
+    bucket_keys_kernel<<<grid_for(C), kBlock, 0, s>>>(C, m->d_cxyz, m->bucket_origin, m->bucket_h, keys_in, ids_in);
+    size_t tmp_bytes = 0;
+    (void)hipcub::DeviceRadixSort::SortPairs(nullptr, tmp_bytes, keys_in, m->d_bkeys, ids_in, m->d_bcells, (int)C, 0, 63,
+                                       s);
+    void* tmp = nullptr;
+    hipError_t e = hipMalloc(&tmp, std::max<size_t>(tmp_bytes, 1));
+    if (e == hipSuccess)
+        e = hipcub::DeviceRadixSort::SortPairs(tmp, tmp_bytes, keys_in, m->d_bkeys, ids_in, m->d_bcells, (int)C, 0, 63,
+                                               s);
+    if (e == hipSuccess) e = hipStreamSynchronize(s);
+    (void)hipFree(tmp); (void)hipFree(keys_in); (void)hipFree(ids_in);
+    if (e != hipSuccess) { free_mesh(m); return fail(MOPS_ERR_HIP, std::string("bucket sort: ") + hipGetErrorString(e)); }
+    m->bytes = acc;
+    *out = m;
+    return MOPS_OK;
+}
+
+void mops_mesh_destroy(mops_mesh* mesh) { free_mesh(mesh); }
+int64_t mops_mesh_bytes(const mops_mesh* mesh) { return mesh ? mesh->bytes : 0; }
+
+mops_status mops_field_create_derived(const mops_mesh* mesh, const double* h_zt, const double* h_vel,
+                                      const double* h_w, void* stream, mops_field** out) {
+    if (!mesh || !out || !h_zt || !h_vel) return fail(MOPS_ERR_INVALID, "mops_field_create_derived: null argument");
+    *out = nullptr;
+    hipStream_t s = (hipStream_t)stream;
+    mops_field* f = new mops_field();
+    f->mesh = mesh; f->V = mesh->V; f->L = mesh->L;
+    const size_t V = (size_t)mesh->V, L = (size_t)mesh->L;
+    mops_status st;
+    if ((st = upload(h_zt, V * L, &f->d_zt, &f->bytes, s)) != MOPS_OK ||
+        (st = upload(h_vel, V * L * 3, &f->d_vel, &f->bytes, s)) != MOPS_OK) { free_field(f); return st; }
+    if (h_w) {
+        if ((st = upload(h_w, V * (L + 1), &f->d_w, &f->bytes, s)) != MOPS_OK) { free_field(f); return st; }
+    } else {
+        if ((st = dmalloc(&f->d_w, V * (L + 1), &f->bytes)) != MOPS_OK) { free_field(f); return st; }
+        HIP_TRY(hipMemsetAsync(f->d_w, 0, V * (L + 1) * sizeof(double), s));
+    }
+    HIP_TRY(hipStreamSynchronize(s));
+    *out = f;
+    return MOPS_OK;
+}
+
+mops_status mops_field_create(const mops_mesh* mesh, const mops_snapshot_desc* desc, void* stream,
+                              mops_field** out) {
+    if (!mesh || !desc || !out) return fail(MOPS_ERR_INVALID, "mops_field_create: null argument");
+    *out = nullptr;
+    if (!desc->h_layer_thickness)
+        return fail(MOPS_ERR_INVALID, "cellLayerThickness is not defined");  // MPASOSolution.cpp:540-544
+    if (!desc->h_zonal_velocity || !desc->h_meridional_velocity)
+        return fail(MOPS_ERR_INVALID, "zonal/meridional velocity required");
+    if (!mesh->d_cov) return fail(MOPS_ERR_INVALID, "mesh has no cellsOnVertex");
+    hipStream_t s = (hipStream_t)stream;
+    const int64_t C = mesh->C, V = mesh->V;
+    const int L = mesh->L;
+    mops_field* f = new mops_field();
+    f->mesh = mesh; f->V = V; f->L = L;
+    double *thick = nullptr, *bot = nullptr, *ssh = nullptr, *zon = nullptr, *mer = nullptr, *wc = nullptr;
+    double *ztc = nullptr, *velc = nullptr;
+    int64_t scratch = 0;
+    mops_status st = MOPS_OK;
+    auto cleanup = [&]() {
+        (void)hipFree(thick); (void)hipFree(bot); (void)hipFree(ssh); (void)hipFree(zon); (void)hipFree(mer); (void)hipFree(wc); (void)hipFree(ztc);
+        (void)hipFree(velc);
+    };
+    do {
+        if ((st = upload(desc->h_layer_thickness, (size_t)(C * L), &thick, &scratch, s)) != MOPS_OK) break;
+        if (desc->h_bottom_depth && (st = upload(desc->h_bottom_depth, (size_t)C, &bot, &scratch, s)) != MOPS_OK) break;
+        if (!desc->h_bottom_depth && desc->h_surface_height &&
+            (st = upload(desc->h_surface_height, (size_t)C, &ssh, &scratch, s)) != MOPS_OK) break;
+        if ((st = upload(desc->h_zonal_velocity, (size_t)(C * L), &zon, &scratch, s)) != MOPS_OK) break;
+        if ((st = upload(desc->h_meridional_velocity, (size_t)(C * L), &mer, &scratch, s)) != MOPS_OK) break;
+        if (desc->h_vert_velocity_top &&
+            (st = upload(desc->h_vert_velocity_top, (size_t)(C * (L + 1)), &wc, &scratch, s)) != MOPS_OK) break;
+        if ((st = dmalloc(&ztc, (size_t)(C * L), &scratch)) != MOPS_OK) break;
+        if ((st = dmalloc(&velc, (size_t)(C * L * 3), &scratch)) != MOPS_OK) break;
+        if ((st = dmalloc(&f->d_zt, (size_t)(V * L), &f->bytes)) != MOPS_OK) break;
+        if ((st = dmalloc(&f->d_vel, (size_t)(V * L * 3), &f->bytes)) != MOPS_OK) break;
+        if ((st = dmalloc(&f->d_w, (size_t)(V * (L + 1)), &f->bytes)) != MOPS_OK) break;
+        cell_ztop_kernel<<<grid_for(C), kBlock, 0, s>>>(C, L, thick, bot, ssh, ztc);
+        cell_to_vertex_kernel<1><<<grid_for(V * L), kBlock, 0, s>>>(V, L, mesh->d_cov, mesh->d_cxyz, mesh->d_vxyz, ztc,
+                                                                   f->d_zt, 0);
+        center_vel_zm_kernel<<<grid_for(C * L), kBlock, 0, s>>>(C, L, mesh->d_cxyz, zon, mer, velc);
+        cell_to_vertex_kernel<3><<<grid_for(V * L), kBlock, 0, s>>>(V, L, mesh->d_cov, mesh->d_cxyz, mesh->d_vxyz,
+                                                                   velc, f->d_vel, 0);
+        if (wc) {
+            cell_to_vertex_kernel<1><<<grid_for(V * (L + 1)), kBlock, 0, s>>>(V, L + 1, mesh->d_cov, mesh->d_cxyz,
+                                                                             mesh->d_vxyz, wc, f->d_w, 0);
+        } else {
+            (void)hipMemsetAsync(f->d_w, 0, (size_t)(V * (L + 1)) * sizeof(double), s);
+        }
+        hipError_t e = hipGetLastError();
+        if (e == hipSuccess) e = hipStreamSynchronize(s);
+        if (e != hipSuccess) { st = fail(MOPS_ERR_HIP, std::string("preprocessing: ") + hipGetErrorString(e)); break; }
+    } while (0);
+    cleanup();
+    if (st != MOPS_OK) { free_field(f); return st; }
+    *out = f;
+    return MOPS_OK;
+}
+
+mops_status mops_cell_to_vertex_attr(const mops_mesh* mesh, const double* d_cell_attr, double* d_vertex_attr,
+                                     void* stream) {
+    if (!mesh || !d_cell_attr || !d_vertex_attr || !mesh->d_cov)
+        return fail(MOPS_ERR_INVALID, "mops_cell_to_vertex_attr: null argument");
+    hipStream_t s = (hipStream_t)stream;
+    cell_to_vertex_kernel<1><<<grid_for(mesh->V * mesh->L), kBlock, 0, s>>>(
+        mesh->V, mesh->L, mesh->d_cov, mesh->d_cxyz, mesh->d_vxyz, d_cell_attr, d_vertex_attr, 1);
+    HIP_TRY(hipGetLastError());
+    return MOPS_OK;
+}
+
+mops_status mops_field_export(const mops_field* f, double* h_zt, double* h_vel, double* h_w, void* stream) {
+    if (!f) return fail(MOPS_ERR_INVALID, "mops_field_export: null field");
+    hipStream_t s = (hipStream_t)stream;
+    const size_t V = (size_t)f->V, L = (size_t)f->L;
+    if (h_zt) HIP_TRY(hipMemcpyAsync(h_zt, f->d_zt, V * L * sizeof(double), hipMemcpyDeviceToHost, s));
+    if (h_vel) HIP_TRY(hipMemcpyAsync(h_vel, f->d_vel, V * L * 3 * sizeof(double), hipMemcpyDeviceToHost, s));
+    if (h_w) HIP_TRY(hipMemcpyAsync(h_w, f->d_w, V * (L + 1) * sizeof(double), hipMemcpyDeviceToHost, s));
+    HIP_TRY(hipStreamSynchronize(s));
+    return MOPS_OK;
+}
+
+void mops_field_destroy(mops_field* field) { free_field(field); }
+int64_t mops_field_bytes(const mops_field* field) { return field ? field->bytes : 0; }
+
+mops_status mops_locate_cells(const mops_mesh* mesh, int64_t n, const double* d_points, int32_t* d_cells,
+                              void* stream) {
+    if (!mesh || n < 0 || (n > 0 && (!d_points || !d_cells)))
+        return fail(MOPS_ERR_INVALID, "mops_locate_cells: invalid argument");
+    if (n == 0) return MOPS_OK;
+    hipStream_t s = (hipStream_t)stream;
+    locate_kernel<<<grid_for(n), kBlock, 0, s>>>(n, d_points, mesh->C, mesh->d_cxyz, mesh->d_bkeys, mesh->d_bcells,
+                                                 mesh->bucket_origin, mesh->bucket_h, d_cells);
+    HIP_TRY(hipGetLastError());
+    return MOPS_OK;
+}
+
+int64_t mops_traj_num_records(const mops_traj_cfg* cfg) {
+    if (!cfg || cfg->record_t <= 0) return 0;
+    return cfg->simulation_duration / cfg->record_t;
+}
+
+int64_t mops_traj_num_steps(const mops_traj_cfg* cfg) {
+    if (!cfg || cfg->delta_t <= 0) return 0;
+    return cfg->simulation_duration / cfg->delta_t;
+}
+
+mops_status mops_traj_advance(const mops_mesh* mesh, const mops_field* front, const mops_field* back,
+                              const mops_traj_cfg* cfg, const mops_particles* p, int64_t step_begin,
+                              int64_t step_end, double* d_records, int64_t record_stride, void* stream) {
+    if (!mesh || !front || !cfg || !p) return fail(MOPS_ERR_INVALID, "mops_traj_advance: invalid inputs");
+    if (cfg->delta_t <= 0 || cfg->record_t <= 0 || cfg->simulation_duration <= 0)
+        return fail(MOPS_ERR_INVALID, "invalid trajectory settings");  // :666-669
+    const int64_t K = mops_traj_num_records(cfg), n_steps = mops_traj_num_steps(cfg);
+    if (K <= 0 || n_steps <= 0) return fail(MOPS_ERR_INVALID, "invalid integration steps");  // :709-712
+    if (front->mesh != mesh || (back && back->mesh != mesh)) return fail(MOPS_ERR_INVALID, "field/mesh mismatch");
+    if (p->n < 0 || record_stride < p->n) return fail(MOPS_ERR_INVALID, "record_stride < n");
+    if (p->n == 0) return MOPS_OK;
+    if (!p->d_x || !p->d_y || !p->d_z || !p->d_depth || !p->d_cell || !p->d_death_step || !d_records)
+        return fail(MOPS_ERR_INVALID, "mops_traj_advance: null device pointer");
+    step_begin = std::max<int64_t>(step_begin, 0);
+    step_end = std::min<int64_t>(step_end, n_steps);
+    if (step_begin >= step_end) return MOPS_OK;
+    if (cfg->delta_t > INT32_MAX) return fail(MOPS_ERR_INVALID, "deltaT too large");
+    TrajArgs a;
+    a.cellrec = mesh->d_cellrec; a.cxyz = mesh->d_cxyz; a.vxyz = mesh->d_vxyz;
+    a.C = (int)mesh->C; a.V = (int)mesh->V; a.L = mesh->L;
+    a.f0 = dev::Field{front->d_zt, front->d_vel, front->d_w};
+    a.f1 = back ? dev::Field{back->d_zt, back->d_vel, back->d_w} : a.f0;
+    a.px = p->d_x; a.py = p->d_y; a.pz = p->d_z; a.depth = p->d_depth; a.cell = p->d_cell; a.death = p->d_death_step;
+    a.n = p->n;
+    a.step_begin = step_begin; a.step_end = step_end; a.n_steps = n_steps;
+    const int dt_sign = (cfg->direction == MOPS_FORWARD) ? 1 : -1;
+    a.delta_t = dt_sign * (int)cfg->delta_t;
+    a.dalpha = (double)a.delta_t / (double)cfg->simulation_duration;
+    if (back) {
+        a.rec_period = cfg->record_t / cfg->delta_t;  // record_interval (:1470)
+    } else {
+        a.rec_period = cfg->record_t / gcd64(cfg->record_t, cfg->delta_t);  // run_time % recordT == 0 (:994)
+    }
+    a.K = K;
+    a.rec = d_records;
+    a.rec_stride = record_stride;
+    const bool euler = (cfg->method == MOPS_EULER);
+    hipStream_t s = (hipStream_t)stream;
+    switch (mesh->maxv) {
+        case 7: launch_traj<7>(a, back != nullptr, euler, s); break;
+        case 12: launch_traj<12>(a, back != nullptr, euler, s); break;
+        default: launch_traj<20>(a, back != nullptr, euler, s); break;
+    }
+    HIP_TRY(hipGetLastError());
+    return MOPS_OK;
+}
+
+mops_status mops_traj_finalize(int64_t n, int64_t K, const double* d_seeds, const double* d_records,
+                               int64_t stride, int32_t pathline, double* d_points, double* d_vel, double* d_tmp,
+                               double* d_sal, double* d_last, void* stream) {
+    if (n < 0 || K <= 0 || !d_seeds || !d_records || !d_points || stride < n)
+        return fail(MOPS_ERR_INVALID, "mops_traj_finalize: invalid argument");
+    if (n == 0) return MOPS_OK;
+    hipStream_t s = (hipStream_t)stream;
+    assemble_kernel<<<grid_for(n), kBlock, 0, s>>>(n, K, d_seeds, d_records, stride, pathline, d_points, d_vel, d_tmp,
+                                                   d_sal);
+    remove_nan_kernel<<<grid_for(n), kBlock, 0, s>>>(n, K + 1, d_points, d_vel, d_tmp, d_sal, d_last);
+    HIP_TRY(hipGetLastError());
+    return MOPS_OK;
+}
+
+mops_status mops_remove_nan_lines(int64_t n, int64_t P, double* d_points, double* d_vel, double* d_tmp, double* d_sal,
+                                  double* d_last, void* stream) {
+    if (n < 0 || P <= 0 || !d_points) return fail(MOPS_ERR_INVALID, "mops_remove_nan_lines: invalid argument");
+    if (n == 0) return MOPS_OK;
+    remove_nan_kernel<<<grid_for(n), kBlock, 0, (hipStream_t)stream>>>(n, P, d_points, d_vel, d_tmp, d_sal, d_last);
+    HIP_TRY(hipGetLastError());
+    return MOPS_OK;
+}
+
+mops_status mops_run_trajectories(const mops_mesh* mesh, const mops_field* front, const mops_field* back,
+                                  const mops_traj_cfg* cfg, int64_t n, const double* h_seeds, const float* h_depths,
+                                  float depth, int32_t* h_cells, double* h_points, double* h_vel, double* h_tmp,
+                                  double* h_sal, double* h_last, double* h_final_pos, float* h_final_depth,
+                                  int32_t* h_death, void* stream) {
+    if (!mesh || !front || !cfg) return fail(MOPS_ERR_INVALID, "invalid inputs");  // :659-662
+    if (n <= 0) return MOPS_OK;                                                      // :663-665 (empty)
+    if (!h_seeds || !h_points) return fail(MOPS_ERR_INVALID, "mops_run_trajectories: null host buffer");
+    if (cfg->delta_t <= 0 || cfg->record_t <= 0 || cfg->simulation_duration <= 0)
+        return fail(MOPS_ERR_INVALID, "invalid trajectory settings");
+    const int64_t K = mops_traj_num_records(cfg), n_steps = mops_traj_num_steps(cfg);
+    if (K <= 0 || n_steps <= 0) return fail(MOPS_ERR_INVALID, "invalid integration steps");
+    hipStream_t s = (hipStream_t)stream;
+    const int64_t P = K + 1;
+    // SoA state + record slab, one allocation
+    double *seeds = nullptr, *x = nullptr, *y = nullptr, *z = nullptr, *rec = nullptr;
+    double *pts = nullptr, *vel = nullptr, *tmp = nullptr, *sal = nullptr, *last = nullptr;
+    float* dep = nullptr;
+    int *cells = nullptr, *death = nullptr;
+    mops_status st = MOPS_OK;
+    std::vector<double> hx((size_t)n), hy((size_t)n), hz((size_t)n);
+    std::vector<float> hd((size_t)n);
+    for (int64_t i = 0; i < n; ++i) {
+        hx[i] = h_seeds[3 * i]; hy[i] = h_seeds[3 * i + 1]; hz[i] = h_seeds[3 * i + 2];
+        hd[i] = h_depths ? h_depths[i] : depth;
+    }
+    auto cleanup = [&]() {
+        (void)hipFree(seeds); (void)hipFree(x); (void)hipFree(y); (void)hipFree(z); (void)hipFree(rec); (void)hipFree(pts); (void)hipFree(vel);
+        (void)hipFree(tmp); (void)hipFree(sal); (void)hipFree(last); (void)hipFree(dep); (void)hipFree(cells); (void)hipFree(death);
+    };
+    do {
+        if ((st = upload(h_seeds, (size_t)(3 * n), &seeds, nullptr, s)) != MOPS_OK) break;
+        if ((st = upload(hx.data(), (size_t)n, &x, nullptr, s)) != MOPS_OK) break;
+        if ((st = upload(hy.data(), (size_t)n, &y, nullptr, s)) != MOPS_OK) break;
+        if ((st = upload(hz.data(), (size_t)n, &z, nullptr, s)) != MOPS_OK) break;
+        if ((st = upload(hd.data(), (size_t)n, &dep, nullptr, s)) != MOPS_OK) break;
+        if ((st = dmalloc(&cells, (size_t)n, nullptr)) != MOPS_OK) break;
+        if ((st = dmalloc(&death, (size_t)n, nullptr)) != MOPS_OK) break;
+        if ((st = dmalloc(&rec, (size_t)(K * 6 * n), nullptr)) != MOPS_OK) break;
+        if ((st = dmalloc(&pts, (size_t)(n * P * 3), nullptr)) != MOPS_OK) break;
+        if ((st = dmalloc(&vel, (size_t)(n * P * 3), nullptr)) != MOPS_OK) break;
+        if ((st = dmalloc(&tmp, (size_t)(n * P), nullptr)) != MOPS_OK) break;
+        if ((st = dmalloc(&sal, (size_t)(n * P), nullptr)) != MOPS_OK) break;
+        if ((st = dmalloc(&last, (size_t)(n * 3), nullptr)) != MOPS_OK) break;
+        hipError_t e = hipMemsetAsync(rec, 0, (size_t)(K * 6 * n) * sizeof(double), s);
+        if (e == hipSuccess) e = hipMemsetAsync(death, 0xff, (size_t)n * sizeof(int), s);  // -1 = alive
+        if (e != hipSuccess) { st = fail(MOPS_ERR_HIP, hipGetErrorString(e)); break; }
+        // default_cell_id: entries < 0 are located (MPASOVisualizerKernels.cpp:683-690)
+        std::vector<int32_t> hc((size_t)n, -1);
+        bool need_locate = (h_cells == nullptr);
+        if (h_cells) {
+            for (int64_t i = 0; i < n; ++i) { hc[i] = h_cells[i]; if (hc[i] < 0) need_locate = true; }
+        }
+        if (need_locate) {
+            int32_t* located = nullptr;
+            if ((st = dmalloc(&located, (size_t)n, nullptr)) != MOPS_OK) break;
+            st = mops_locate_cells(mesh, n, seeds, located, s);
+            std::vector<int32_t> hl((size_t)n);
+            if (st == MOPS_OK) {
+                e = hipMemcpyAsync(hl.data(), located, (size_t)n * sizeof(int32_t), hipMemcpyDeviceToHost, s);
+                if (e == hipSuccess) e = hipStreamSynchronize(s);
+                if (e != hipSuccess) st = fail(MOPS_ERR_HIP, hipGetErrorString(e));
+            }
+            (void)hipFree(located);
+            if (st != MOPS_OK) break;
+            for (int64_t i = 0; i < n; ++i) if (hc[i] < 0) hc[i] = hl[i];
+            if (h_cells) for (int64_t i = 0; i < n; ++i) h_cells[i] = hc[i];
+        }
+        e = hipMemcpyAsync(cells, hc.data(), (size_t)n * sizeof(int32_t), hipMemcpyHostToDevice, s);
+        if (e != hipSuccess) { st = fail(MOPS_ERR_HIP, hipGetErrorString(e)); break; }
+        mops_particles prt{n, x, y, z, dep, cells, death};
+        if ((st = mops_traj_advance(mesh, front, back, cfg, &prt, 0, n_steps, rec, n, stream)) != MOPS_OK) break;
+        if ((st = mops_traj_finalize(n, K, seeds, rec, n, back ? 1 : 0, pts, vel, tmp, sal, last, stream)) != MOPS_OK)
+            break;
+        e = hipMemcpyAsync(h_points, pts, (size_t)(n * P * 3) * sizeof(double), hipMemcpyDeviceToHost, s);
+        if (e == hipSuccess && h_vel) e = hipMemcpyAsync(h_vel, vel, (size_t)(n * P * 3) * sizeof(double), hipMemcpyDeviceToHost, s);
+        if (e == hipSuccess && h_tmp) e = hipMemcpyAsync(h_tmp, tmp, (size_t)(n * P) * sizeof(double), hipMemcpyDeviceToHost, s);
+        if (e == hipSuccess && h_sal) e = hipMemcpyAsync(h_sal, sal, (size_t)(n * P) * sizeof(double), hipMemcpyDeviceToHost, s);
+        if (e == hipSuccess && h_last) e = hipMemcpyAsync(h_last, last, (size_t)(n * 3) * sizeof(double), hipMemcpyDeviceToHost, s);
+        if (e == hipSuccess && h_final_depth) e = hipMemcpyAsync(h_final_depth, dep, (size_t)n * sizeof(float), hipMemcpyDeviceToHost, s);
+        if (e == hipSuccess && h_death) e = hipMemcpyAsync(h_death, death, (size_t)n * sizeof(int32_t), hipMemcpyDeviceToHost, s);
+        if (e == hipSuccess && h_final_pos) {
+            e = hipMemcpyAsync(hx.data(), x, (size_t)n * sizeof(double), hipMemcpyDeviceToHost, s);
+            if (e == hipSuccess) e = hipMemcpyAsync(hy.data(), y, (size_t)n * sizeof(double), hipMemcpyDeviceToHost, s);
+            if (e == hipSuccess) e = hipMemcpyAsync(hz.data(), z, (size_t)n * sizeof(double), hipMemcpyDeviceToHost, s);
+        }
+        if (e == hipSuccess) e = hipStreamSynchronize(s);
+        if (e != hipSuccess) { st = fail(MOPS_ERR_HIP, hipGetErrorString(e)); break; }
+        if (h_final_pos)
+            for (int64_t i = 0; i < n; ++i) {
+                h_final_pos[3 * i] = hx[i]; h_final_pos[3 * i + 1] = hy[i]; h_final_pos[3 * i + 2] = hz[i];
+            }
+    } while (0);
+    cleanup();
+    return st;
+}
+
+}  // extern "C"

@@ -1,0 +1,187 @@
+"""GPU parity: the HIP engine (through the C ABI) against the CPU oracle.
+
+Tolerance (north_star): trajectory points within 1e-6 rad of the reference
+on identical seeds; death steps and cells identical.  Every comparison also
+reports the bit-exact fraction -- the engine uses the reference's operation
+order with FMA contraction off, so almost all points are expected to be
+bit-identical (device sin/cos may differ from glibc in the last ulp).
+"""
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+TOL_RAD = 1e-6
+
+
+def ang_err(a, b):
+    na = np.linalg.norm(a, axis=-1)
+    nb = np.linalg.norm(b, axis=-1)
+    both = (na > 0) & (nb > 0) & np.isfinite(na) & np.isfinite(nb)
+    c = np.sum(a * b, -1) / np.where(both, na * nb, 1.0)
+    ang = np.arccos(np.clip(c, -1.0, 1.0))
+    return np.where(both, ang, 0.0), both
+
+
+def assert_lines_match(got, ref, label):
+    assert np.array_equal(got["death_step"], ref["death"]), f"{label}: death steps differ"
+    for key in ("points", "lastPoint"):
+        a, b = got[key], ref[key]
+        # zero (never-written) slots and NaN padding must coincide exactly
+        assert np.array_equal(np.linalg.norm(a, axis=-1) == 0, np.linalg.norm(b, axis=-1) == 0), f"{label} {key} zeros"
+        assert np.array_equal(np.isfinite(a), np.isfinite(b)), f"{label} {key} NaN pattern"
+        e, _ = ang_err(a, b)
+        assert e.max() < TOL_RAD, f"{label} {key}: max angular error {e.max()} rad"
+        rel = np.abs(np.linalg.norm(a, axis=-1) - np.linalg.norm(b, axis=-1))
+        assert np.nanmax(rel) < 1e-3, f"{label} {key}: radius differs by {np.nanmax(rel)} m"
+    v_ok = np.isfinite(ref["velocity"]) & np.isfinite(got["velocity"])
+    assert np.allclose(got["velocity"][v_ok], ref["velocity"][v_ok], rtol=1e-9, atol=1e-12), f"{label}: velocity"
+    assert np.allclose(got["final_depth"], ref["final_depth"], rtol=1e-6, atol=1e-3), f"{label}: depth"
+    exact = np.mean(np.all(got["points"] == ref["points"], axis=-1))
+    return exact
+
+
+@pytest.fixture(scope="module")
+def dev_small(gpu, engine_lib, small_case):
+    from mops_amd.engine import DeviceField, DeviceMesh
+    mesh, s0, s1 = small_case
+    dm = DeviceMesh.from_mesh(mesh)
+    return dm, DeviceField.from_snapshot(dm, s0), DeviceField.from_snapshot(dm, s1)
+
+
+@pytest.fixture(scope="module")
+def ref_small(oracle_lib, small_case):
+    mesh, s0, s1 = small_case
+    return oracle_lib.preprocess(mesh, s0), oracle_lib.preprocess(mesh, s1)
+
+
+def test_device_math_matches_host(gpu):
+    """sqrt / division must be correctly rounded on gfx950 (bit parity)."""
+    import torch
+    rng = np.random.default_rng(0)
+    x = rng.uniform(1e-3, 1e14, 200000)
+    t = torch.as_tensor(x, device=gpu)
+    assert np.array_equal(torch.sqrt(t).cpu().numpy(), np.sqrt(x))
+    y = rng.uniform(-1e7, 1e7, 200000)
+    assert np.array_equal((torch.as_tensor(y, device=gpu) / t).cpu().numpy(), y / x)
+
+
+def test_preprocessing_bitwise(dev_small, ref_small, small_case):
+    mesh, s0, s1 = small_case
+    _, f0, _ = dev_small
+    r0, _ = ref_small
+    zt, ve, w = f0.export()
+    assert np.array_equal(zt, r0.vertex_ztop)
+    assert np.array_equal(ve, r0.vertex_vel)
+    assert np.array_equal(w, r0.vertex_w)
+
+
+def test_locate_matches_bruteforce(gpu, dev_small, small_case, oracle_lib):
+    import torch
+    from mops_amd import synth
+    mesh, _, _ = small_case
+    dm, _, _ = dev_small
+    pts = np.concatenate([synth.uniform_band_seeds(3000, seed=3, max_abs_lat=89.0),
+                          synth.lattice_seeds(21, 21, (-60, 60), (-180, 180)),
+                          mesh.cellCoord[:50] * 1.0])           # exact cell centres
+    ref = oracle_lib.knn(mesh, pts)
+    d = torch.as_tensor(pts, device=gpu)
+    out = torch.empty(len(pts), dtype=torch.int32, device=gpu)
+    dm.locate(d.data_ptr(), out.data_ptr(), len(pts))
+    torch.cuda.synchronize()
+    assert np.array_equal(out.cpu().numpy(), ref)
+
+
+@pytest.mark.parametrize("method", ["euler", "rk4"])
+@pytest.mark.parametrize("direction", ["forward", "backward"])
+def test_streamline_parity(dev_small, ref_small, small_case, oracle_lib, method, direction):
+    from mops_amd import synth
+    from mops_amd.engine import TrajectoryConfig, run_trajectories
+    mesh, _, _ = small_case
+    dm, f0, _ = dev_small
+    r0, _ = ref_small
+    seeds = np.concatenate([synth.lattice_seeds(11, 11, (-40.0, 40.0), (-60.0, 60.0)),
+                            synth.uniform_band_seeds(400, seed=11)])
+    depth = 800.0
+    cfg = TrajectoryConfig(deltaT=120, simulationDuration=86400, recordT=3600, depth=depth,
+                           method=1 if method == "euler" else 0, direction=0 if direction == "forward" else 1)
+    got = run_trajectories(dm, f0, None, cfg, seeds)
+    ref = oracle_lib.run(mesh, r0, None, seeds, depth=depth, delta_t=120, duration=86400, record_t=3600,
+                         euler=(method == "euler"), backward=(direction == "backward"), cells=got["cells"])
+    exact = assert_lines_match(got, ref, f"streamline {method} {direction}")
+    print(f"bit-exact points: {exact:.4f}")
+
+
+@pytest.mark.parametrize("method", ["euler", "rk4"])
+def test_pathline_parity(dev_small, ref_small, small_case, oracle_lib, method):
+    from mops_amd import synth
+    from mops_amd.engine import TrajectoryConfig, run_trajectories
+    mesh, _, _ = small_case
+    dm, f0, f1 = dev_small
+    r0, r1 = ref_small
+    seeds = synth.uniform_band_seeds(500, seed=5)
+    rng = np.random.default_rng(9)
+    depths = rng.uniform(5.0, 1500.0, len(seeds)).astype(np.float32)
+    cfg = TrajectoryConfig(deltaT=60, simulationDuration=86400, recordT=3600, depth=0.0,
+                           method=1 if method == "euler" else 0)
+    got = run_trajectories(dm, f0, f1, cfg, seeds, depths=depths)
+    ref = oracle_lib.run(mesh, r0, r1, seeds, depths=depths, delta_t=60, duration=86400, record_t=3600,
+                         euler=(method == "euler"), cells=got["cells"])
+    exact = assert_lines_match(got, ref, f"pathline {method}")
+    assert np.array_equal(got["temperature"], ref["temperature"])  # Q9: velocity x
+    assert np.array_equal(got["salinity"], ref["salinity"])        # Q9: velocity y
+    print(f"bit-exact points: {exact:.4f}")
+
+
+def test_record_rules_odd_periods(dev_small, ref_small, small_case, oracle_lib):
+    """recordT not a multiple of deltaT (streamline run_time % recordT rule)."""
+    from mops_amd import synth
+    from mops_amd.engine import TrajectoryConfig, run_trajectories
+    mesh, _, _ = small_case
+    dm, f0, f1 = dev_small
+    r0, r1 = ref_small
+    seeds = synth.uniform_band_seeds(200, seed=21)
+    for back, rr in ((None, None), (f1, r1)):
+        cfg = TrajectoryConfig(deltaT=120, simulationDuration=7200, recordT=300, depth=100.0)
+        got = run_trajectories(dm, f0, back, cfg, seeds)
+        ref = oracle_lib.run(mesh, r0, rr, seeds, depth=100.0, delta_t=120, duration=7200, record_t=300,
+                             cells=got["cells"])
+        assert_lines_match(got, ref, "odd record period")
+
+
+def test_segmented_advance_equals_single(gpu, dev_small, small_case):
+    import torch
+    from mops_amd import synth
+    from mops_amd.engine import ParticleSet, TrajectoryConfig
+    dm, f0, _ = dev_small
+    seeds = synth.uniform_band_seeds(1000, seed=8)
+    cfg = TrajectoryConfig(deltaT=120, simulationDuration=86400, recordT=3600, depth=500.0, method=0)
+    a = ParticleSet(dm, seeds, 500.0, cfg)
+    a.advance(f0, None, 0, cfg.n_steps)
+    b = ParticleSet(dm, seeds, 500.0, cfg)
+    for s in range(0, cfg.n_steps, 37):
+        b.advance(f0, None, s, min(s + 37, cfg.n_steps))
+    torch.cuda.synchronize()
+    assert torch.equal(a.records, b.records)
+    assert torch.equal(a.x, b.x) and torch.equal(a.death, b.death) and torch.equal(a.depth, b.depth)
+
+
+def test_medium_mesh_l60_parity(gpu, engine_lib, medium_case, oracle_lib):
+    """EC30to60-like vertical grid (60 levels): exercises the streaming bracket."""
+    from mops_amd import synth
+    from mops_amd.engine import DeviceField, DeviceMesh, TrajectoryConfig, run_trajectories
+    mesh, s0, s1 = medium_case
+    dm = DeviceMesh.from_mesh(mesh)
+    f0 = DeviceField.from_snapshot(dm, s0)
+    r0 = oracle_lib.preprocess(mesh, s0)
+    zt, ve, w = f0.export()
+    assert np.array_equal(zt, r0.vertex_ztop) and np.array_equal(ve, r0.vertex_vel)
+    seeds = synth.uniform_band_seeds(2000, seed=12345)
+    rng = np.random.default_rng(1)
+    depths = rng.choice(np.array([0.0, 20.0, 800.0, 2500.0, 5000.0], dtype=np.float32), len(seeds))
+    for method in (1, 0):
+        cfg = TrajectoryConfig(deltaT=120, simulationDuration=43200, recordT=3600, depth=0.0, method=method)
+        got = run_trajectories(dm, f0, None, cfg, seeds, depths=depths)
+        ref = oracle_lib.run(mesh, r0, None, seeds, depths=depths, delta_t=120, duration=43200, record_t=3600,
+                             euler=(method == 1), cells=got["cells"])
+        assert_lines_match(got, ref, f"medium method={method}")
