@@ -1,0 +1,244 @@
+#!/usr/bin/env python3
+"""Benchmark: particle-steps/sec of the MI355X StreamLine hot path.
+
+Workload (BASELINE.json configs[1]): EC30to60-class mesh (synthetic, ~236k
+ocean cells, 60 levels), 1e6 particles per GPU, fixed depth 800 m,
+dt = 120 s, 1-day streamline (720 steps, Euler = the reference default),
+records every 3600 s.  One bench "step" = one complete StreamLine call on
+the rank's particle shard: seed location, 720 integration steps in 24
+record segments and -- for N > 1 -- an RCCL all-gather of each record slab
+over xGMI on a side stream, overlapped with the next segment's kernel.
+
+Inputs (mesh, fields, seeds) are resident in HBM before the timed region.
+Rank 0 prints one JSON line (driver contract).
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import math
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+PEAK_HBM_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md)
+
+
+def parse():
+    p = argparse.ArgumentParser()
+    p.add_argument("--gpus", type=int, default=1)
+    p.add_argument("--steps", type=int, default=3)
+    p.add_argument("--warmup", type=int, default=1)
+    p.add_argument("--particles", type=int, default=1_000_000, help="particles per GPU")
+    p.add_argument("--freq", type=int, default=158, help="icosahedral frequency (158 -> ~236k ocean cells)")
+    p.add_argument("--levels", type=int, default=60)
+    p.add_argument("--depth", type=float, default=800.0)
+    p.add_argument("--dt", type=int, default=120)
+    p.add_argument("--duration", type=int, default=86400)
+    p.add_argument("--record", type=int, default=3600)
+    p.add_argument("--method", choices=["euler", "rk4"], default="euler")
+    p.add_argument("--no-cpu-baseline", action="store_true")
+    p.add_argument("--cpu-seconds", type=float, default=12.0, help="target CPU-baseline sample length")
+    return p.parse_args()
+
+
+def algorithmic_bytes_per_pstep(nv: float, L: int, S: int = 1) -> float:
+    """one compulsory fetch of the particle's cell stencil per step."""
+    return (4 + 4 * nv + 4 * nv + 24 * nv + 24 * (nv + 1) + S * (8 * nv * L + 2 * 24 * nv + 2 * 8 * nv) + 32)
+
+
+def main():
+    args = parse()
+    import torch
+    import torch.distributed as dist
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    torch.cuda.set_device(local_rank)
+    dev = torch.device("cuda", local_rank)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=dev)
+
+    from mops_amd import synth
+    from mops_amd.engine import DeviceField, DeviceMesh, ParticleSet, TrajectoryConfig
+
+    mesh = synth.make_mesh(args.freq, n_levels=args.levels)
+    snap = synth.make_snapshot(mesh, timestep=0)
+    dmesh = DeviceMesh.from_mesh(mesh)
+    dfield = DeviceField.from_snapshot(dmesh, snap)
+    # seeds: uniform on |lat| < 70 deg, rejected on land, one shard per rank
+    rng_seed = 12345 + rank
+    seeds = synth.uniform_band_seeds(int(args.particles * 1.25) + 64, seed=rng_seed)
+    r = np.linalg.norm(seeds, axis=1)
+    lat = np.arcsin(seeds[:, 2] / r); lon = np.arctan2(seeds[:, 1], seeds[:, 0])
+    seeds = seeds[~synth._land_mask(lat, lon, "continents")][: args.particles]
+    n = seeds.shape[0]
+    cfg = TrajectoryConfig(deltaT=args.dt, simulationDuration=args.duration, recordT=args.record, depth=args.depth,
+                           method=1 if args.method == "euler" else 0)
+    ps = ParticleSet(dmesh, seeds, args.depth, cfg, device=dev)
+    period = ps.record_period(pathline=False)
+    n_steps = cfg.n_steps
+    bounds = list(range(0, n_steps, period)) + [n_steps]
+    segments = [(bounds[i], bounds[i + 1]) for i in range(len(bounds) - 1)]
+    compute = torch.cuda.Stream(dev)
+    comm = torch.cuda.Stream(dev)
+    gathered = None
+    if world > 1:
+        gathered = torch.empty((ps.K, world, 6, n), dtype=torch.float64, device=dev)
+    seeds_dev = ps.seeds
+
+    kernel_ms = []
+
+    def one_call(timed: bool):
+        """One StreamLine call on this rank's shard (device resident)."""
+        with torch.cuda.stream(compute):
+            ps.reset(depth=args.depth)
+            dmesh.locate(seeds_dev.data_ptr(), ps.cell.data_ptr(), n, stream=compute)
+            ps.reorder(stream=compute)
+            for (s0, s1) in segments:
+                if timed:
+                    e0 = torch.cuda.Event(enable_timing=True); e1 = torch.cuda.Event(enable_timing=True)
+                    e0.record(compute)
+                ps.advance(dfield, None, s0, s1, stream=compute)
+                if timed:
+                    e1.record(compute)
+                    kernel_ms.append((e0, e1))
+                if world > 1:
+                    k = s1 // period - 1
+                    if 0 <= k < ps.K:
+                        done = torch.cuda.Event()
+                        done.record(compute)
+                        comm.wait_event(done)
+                        with torch.cuda.stream(comm):
+                            dist.all_gather_into_tensor(gathered[k].view(-1), ps.records[k].view(-1))
+        compute.synchronize()
+        comm.synchronize()
+
+    for _ in range(args.warmup):
+        one_call(False)
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        one_call(True)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    torch.cuda.synchronize()
+
+    # attempted particle-steps (a step counts once its velocity evaluation ran)
+    death = ps.death.to(torch.int64)
+    attempted = torch.where(death < 0, torch.full_like(death, n_steps), death + 1).sum().item()
+    dead = int((death >= 0).sum().item())
+    kms = [a.elapsed_time(b) for (a, b) in kernel_ms]
+    avg_kernel_s = (sum(kms) / len(kms)) / 1e3 if kms else float("nan")
+    stats = torch.tensor([elapsed, float(attempted), float(n), float(dead)], dtype=torch.float64, device=dev)
+    if world > 1:
+        mx = stats.clone(); dist.all_reduce(mx, op=dist.ReduceOp.MAX)
+        sm = stats.clone(); dist.all_reduce(sm, op=dist.ReduceOp.SUM)
+        elapsed = mx[0].item()
+        attempted_all, n_all, dead_all = sm[1].item(), sm[2].item(), sm[3].item()
+    else:
+        attempted_all, n_all, dead_all = float(attempted), float(n), float(dead)
+
+    value = attempted_all * args.steps / elapsed
+    nv_mean = float(np.mean(mesh.nEdgesOnCell.astype(np.float64)))
+    B = algorithmic_bytes_per_pstep(nv_mean, mesh.nVertLevels, 1)
+    psteps_per_launch = attempted / len(segments)
+    achieved = B * psteps_per_launch / avg_kernel_s / 1e9
+    traffic = None
+    pmc_path = os.path.join(ROOT, "profiles", "pmc_traffic.json")
+    if os.path.exists(pmc_path):
+        try:
+            pm = json.load(open(pmc_path))
+            if pm.get("workload") == f"ec30to60_streamline_{args.method}_{args.particles}":
+                traffic = pm.get("bytes_per_launch")
+        except Exception:
+            traffic = None
+
+    cpu = None
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        cpu = cpu_baseline(mesh, snap, seeds, ps.cell.cpu().numpy(), args, n_steps)
+
+    if rank == 0:
+        line = {
+            "metric": "particle-steps/sec",
+            "value": value,
+            "unit": "particle-steps/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": elapsed / args.steps * 1e3,
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "f64",
+            "data": "synthetic (icosahedral-dual Voronoi mesh, analytic flow; no MPAS files offline)",
+            "config": {
+                "workload": "EC30to60-class streamline, 1e6 particles/GPU, depth 800 m, dt 120 s, 1 day",
+                "cells": mesh.nCells, "vertices": mesh.nVertices, "levels": mesh.nVertLevels,
+                "particles_per_gpu": n, "particles_total": int(n_all), "integration_steps": n_steps,
+                "records": ps.K, "method": args.method, "parallelism": f"particle-shard x{world}",
+                "record_gather": "rccl all_gather per record instant (side stream)" if world > 1 else "none",
+            },
+            "nominal_particle_steps_per_call": n_all * n_steps,
+            "attempted_particle_steps_per_call": attempted_all,
+            "dead_fraction": dead_all / max(n_all, 1),
+            "roofline": {
+                "bound": "hbm",
+                "achieved": achieved,
+                "peak": PEAK_HBM_GBS,
+                "unit": "GB/s",
+                "frac": achieved / PEAK_HBM_GBS,
+                "traffic": traffic,
+                "kernel": "traj_kernel<7,false,true> (streamline Euler)" if args.method == "euler"
+                else "traj_kernel<7,false,false> (streamline RK4)",
+                "algorithmic_bytes_per_particle_step": B,
+                "particle_steps_per_launch": psteps_per_launch,
+                "avg_launch_ms": avg_kernel_s * 1e3,
+            },
+            "cpu_baseline": cpu,
+        }
+        print(json.dumps(line))
+    if world > 1:
+        dist.destroy_process_group()
+
+
+def cpu_baseline(mesh, snap, seeds, cells, args, n_steps):
+    """The CPU oracle (port of the TBB path) on this host's cores, bounded sample."""
+    try:
+        from oracle import oracle as O
+    except Exception as e:  # pragma: no cover
+        return {"error": f"oracle unavailable: {e}"}
+    threads = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or (os.cpu_count() or 1)
+    threads = max(1, min(threads, os.cpu_count() or 1))
+    derived = O.preprocess(mesh, snap)
+    euler = args.method == "euler"
+    # calibrate on a small sample, then size the timed sample to ~cpu_seconds
+    n0 = min(4000, len(seeds))
+    t = time.perf_counter()
+    O.run(mesh, derived, None, seeds[:n0], depth=args.depth, delta_t=args.dt, duration=args.duration,
+          record_t=args.record, euler=euler, cells=cells[:n0], n_threads=threads, finalize=False)
+    rate = n0 * n_steps / max(time.perf_counter() - t, 1e-6)
+    n1 = int(min(len(seeds), max(n0, rate * args.cpu_seconds / n_steps)))
+    t = time.perf_counter()
+    out = O.run(mesh, derived, None, seeds[:n1], depth=args.depth, delta_t=args.dt, duration=args.duration,
+                record_t=args.record, euler=euler, cells=cells[:n1], n_threads=threads, finalize=False)
+    dt = time.perf_counter() - t
+    death = out["death"].astype(np.int64)
+    attempted = np.where(death < 0, n_steps, death + 1).sum()
+    return {"value": float(attempted / dt), "unit": "particle-steps/s", "cores": threads, "kind": "port",
+            "sample": f"{n1} of the same seeds x {n_steps} steps ({args.method}), same mesh/field, "
+                      f"OpenMP schedule(dynamic,16) over particles; {dt:.1f} s"}
+
+
+if __name__ == "__main__":
+    main()

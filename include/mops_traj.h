@@ -89,6 +89,9 @@ typedef struct {
     float* d_depth;                      /* effective_depths (float, as the reference) */
     int32_t* d_cell;                     /* in: seed cell (default_cell_id), then current cell */
     int32_t* d_death_step;               /* out: -1 alive, else the step it died at */
+    const int32_t* d_order;              /* optional processing order (slot -> particle index),
+                                            from mops_order_particles; NULL = identity.  Only
+                                            affects speed, never results. */
 } mops_particles;
 
 const char* mops_last_error(void);
@@ -136,6 +139,13 @@ int64_t mops_field_bytes(const mops_field* field);
  * 1-NN).  Ties resolve to the smallest cell index. */
 mops_status mops_locate_cells(const mops_mesh* mesh, int64_t n, const double* d_points, int32_t* d_cells,
                               void* stream);
+
+/* Locality order for n particles: sorts particle indices by a Morton key
+ * of their current cell centre, so a wavefront's lanes share cell stencils
+ * (no reference counterpart: the reference processes particles in index
+ * order).  d_cell [n] -> d_order [n] (device). */
+mops_status mops_order_particles(const mops_mesh* mesh, int64_t n, const int32_t* d_cell, int32_t* d_order,
+                                 void* stream);
 
 /* ---- trajectory hot path (device-resident) ----------------------------- */
 

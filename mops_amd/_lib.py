@@ -18,7 +18,7 @@ EXPORTED = (
     "mops_mesh_create", "mops_mesh_destroy", "mops_mesh_bytes",
     "mops_field_create", "mops_field_create_derived", "mops_field_export", "mops_cell_to_vertex_attr",
     "mops_field_destroy", "mops_field_bytes",
-    "mops_locate_cells",
+    "mops_locate_cells", "mops_order_particles",
     "mops_traj_num_records", "mops_traj_num_steps", "mops_traj_advance", "mops_traj_finalize",
     "mops_remove_nan_lines", "mops_run_trajectories",
 )
@@ -48,7 +48,8 @@ class TrajCfg(C.Structure):
 
 class Particles(C.Structure):
     _fields_ = [("n", C.c_int64), ("d_x", C.c_void_p), ("d_y", C.c_void_p), ("d_z", C.c_void_p),
-                ("d_depth", C.c_void_p), ("d_cell", C.c_void_p), ("d_death_step", C.c_void_p)]
+                ("d_depth", C.c_void_p), ("d_cell", C.c_void_p), ("d_death_step", C.c_void_p),
+                ("d_order", C.c_void_p)]
 
 
 class MopsError(RuntimeError):
@@ -82,6 +83,7 @@ def load(path: str | None = None):
     lib.mops_field_destroy.argtypes = [P]; lib.mops_field_destroy.restype = None
     lib.mops_field_bytes.argtypes = [P]; lib.mops_field_bytes.restype = I64
     lib.mops_locate_cells.argtypes = [P, I64, P, P, P]; lib.mops_locate_cells.restype = st
+    lib.mops_order_particles.argtypes = [P, I64, P, P, P]; lib.mops_order_particles.restype = st
     lib.mops_traj_num_records.argtypes = [P]; lib.mops_traj_num_records.restype = I64
     lib.mops_traj_num_steps.argtypes = [P]; lib.mops_traj_num_steps.restype = I64
     lib.mops_traj_advance.argtypes = [P, P, P, P, P, I64, I64, P, I64, P]; lib.mops_traj_advance.restype = st

@@ -76,6 +76,10 @@ struct mops_mesh {
     double bucket_h = 0.0, bucket_origin = 0.0;
     uint64_t* d_bkeys = nullptr;  // sorted bucket keys [C]
     int* d_bcells = nullptr;      // cell ids in key order [C]
+    uint64_t* d_cell_key = nullptr;  // Morton key of each cell centre (particle locality order)
+    // grow-only scratch for mops_order_particles (not re-entrant, like the reference's global app)
+    mutable void* d_scratch = nullptr;
+    mutable size_t scratch_bytes = 0;
     int64_t bytes = 0;
 };
 
@@ -86,6 +90,7 @@ struct mops_field {
     double* d_zt = nullptr;   // cellVertexZTop [V][L]
     double* d_vel = nullptr;  // cellVertexVelocity [V][L][3]
     double* d_w = nullptr;    // cellVertexVertVelocity [V][L+1]
+    uint8_t* d_mono = nullptr;  // [C] 1 = every vertex column of the cell strictly decreasing (margin)
     int64_t bytes = 0;
 };
 
@@ -138,6 +143,7 @@ template <int MAXV>
 struct Cell {
     int id;
     int nv;
+    bool mono0, mono1;  // fast-path flags of the cell for the front / back field
     int vid[MAXV];
     int coc[MAXV];
     double x[MAXV], y[MAXV], z[MAXV];
@@ -146,7 +152,10 @@ struct Cell {
 
 template <int MAXV>
 __device__ __forceinline__ void load_cell(Cell<MAXV>& c, int cell, const int* __restrict__ cellrec,
-                                          const double4* __restrict__ vxyz) {
+                                          const double4* __restrict__ vxyz, const uint8_t* __restrict__ mono0,
+                                          const uint8_t* __restrict__ mono1) {
+    c.mono0 = mono0[cell] != 0;
+    c.mono1 = mono1[cell] != 0;
     constexpr int REC = ((1 + 2 * MAXV) + 3) / 4 * 4;
     const int* r = cellrec + (int64_t)cell * REC;
     int buf[REC];
@@ -330,6 +339,99 @@ __device__ __forceinline__ int bracket_scan(const Cell<MAXV>& c, const double* w
     return layer;
 }
 
+// Fast, exact bracket for cells whose vertex columns are all strictly
+// decreasing by >= 1e-6 m (field flag d_mono) when every Wachspress weight is
+// finite.  The weights are then >= 0 (triangle areas are sqrt's) and sum to
+// 1 +- nv ulp, so the interpolated column is strictly decreasing with a margin
+// far above its rounding error (|z| <= 1e6 m: error < 1e-9): the
+// reference's fix-up never fires and z'_k = z_k, computable level by level.
+// a and b (see bracket_scan) are then found by walking from the particle's
+// previous layer (`hint`); typically two levels plus the surface level are
+// read instead of the whole column.  Any hint gives the same result.
+template <int MAXV, bool PATH>
+__device__ __forceinline__ int bracket_mono(const Cell<MAXV>& c, const double* w, const double* __restrict__ zt,
+                                            int L, double d, int& hint, double& zdn, double& zup) {
+    const double eps = 1e-8;
+    const double z0 = col<MAXV>(c, w, zt, L, 0);
+    if (d > z0 + eps) {  // above the surface (PATH: see DESIGN.md Q4)
+        zdn = col<MAXV>(c, w, zt, L, 1); zup = z0; hint = 1;
+        return 1;
+    }
+    int h = hint;
+    if (h < 1 || h > L - 1) {  // no hint: lower_bound of Q over [1, L-1] by bisection
+        int lo = 1, hi = L;
+        while (lo < hi) {
+            const int mid = (lo + hi) >> 1;
+            if (d >= col<MAXV>(c, w, zt, L, mid) - eps) hi = mid; else lo = mid + 1;
+        }
+        h = (lo <= L - 1) ? lo : L - 1;
+    }
+    int a;
+    double za, zam1;  // z_a, z_{a-1}
+    const double zh = col<MAXV>(c, w, zt, L, h);
+    if (d >= zh - eps) {  // a <= h: walk towards the surface
+        int k = h;
+        double zk = zh;
+        double zkm1 = (k == 1) ? z0 : col<MAXV>(c, w, zt, L, k - 1);
+        while (k > 1 && d >= zkm1 - eps) {
+            --k;
+            zk = zkm1;
+            zkm1 = (k == 1) ? z0 : col<MAXV>(c, w, zt, L, k - 1);
+        }
+        a = k; za = zk; zam1 = zkm1;
+    } else {  // a > h: walk towards the bottom
+        int k = h;
+        double zk = zh, zprev = zh;
+        bool found = false;
+        while (k < L - 1) {
+            ++k;
+            zprev = zk;
+            zk = col<MAXV>(c, w, zt, L, k);
+            if (d >= zk - eps) { found = true; break; }
+        }
+        if (!found) {  // Q(L-1) false  <=>  d < z_{L-1} - eps: the "below the bottom" branch
+            const double zlm1 = (k == h) ? ((L - 2 == 0) ? z0 : col<MAXV>(c, w, zt, L, L - 2)) : zprev;
+            zdn = zk; zup = zlm1; hint = L - 1;
+            return L - 1;
+        }
+        a = k; za = zk; zam1 = zprev;
+    }
+    // b = last k with P(k) = d <= z_{k-1} + eps; P(a) holds (a == 1: not above
+    // the surface; a > 1: !Q(a-1))
+    int b = a;
+    double zb = za, zbm1 = zam1;
+    while (b < L - 1 && d <= zb + eps) {
+        const double zn = col<MAXV>(c, w, zt, L, b + 1);
+        zbm1 = zb; zb = zn; ++b;
+    }
+    int layer;
+    if (PATH) {
+        layer = a;  // linear scan: first k with P && Q
+    } else {        // the reference's binary search, driven by (a, b)
+        int lo = 1, hi = L - 1, ans = 1;
+        while (lo <= hi) {
+            const int mid = (lo + hi) >> 1;
+            if (mid >= a && mid <= b) { ans = mid; break; }
+            if (mid > b) hi = mid - 1; else lo = mid + 1;
+        }
+        layer = ans;
+    }
+    if (layer == a) { zdn = za; zup = zam1; }
+    else if (layer == b) { zdn = zb; zup = zbm1; }
+    else { zdn = col<MAXV>(c, w, zt, L, layer); zup = col<MAXV>(c, w, zt, L, layer - 1); }
+    hint = layer;
+    return layer;
+}
+
+template <int MAXV>
+__device__ __forceinline__ bool weights_finite(const Cell<MAXV>& c, const double* w) {
+    bool ok = true;
+#pragma unroll
+    for (int i = 0; i < MAXV; ++i)
+        if (i < c.nv) ok = ok && isfinite(w[i]);
+    return ok;
+}
+
 template <int MAXV>
 __device__ __forceinline__ void vel_at(const Cell<MAXV>& c, const double* w, const double* __restrict__ vel, int L,
                                        int layer, double& vx, double& vy, double& vz) {
@@ -364,11 +466,14 @@ struct Field {
 // streamline calc_velocity_at (MPASOVisualizerKernels.cpp:740-872)
 template <int MAXV>
 __device__ __forceinline__ bool eval_stream(const Cell<MAXV>& c, int L, int V, const Field& f, double px, double py,
-                                            double pz, double d, double& hx, double& hy, double& hz, double& wv) {
+                                            double pz, double d, int& hint, double& hx, double& hy, double& hz,
+                                            double& wv) {
     double w[MAXV];
     if (!weights<MAXV>(c, L, V, px, py, pz, w)) return false;
     double zdn, zup;
-    const int layer = bracket_scan<MAXV, false>(c, w, f.zt, L, d, zdn, zup);
+    const int layer = (c.mono0 && weights_finite<MAXV>(c, w))
+                          ? bracket_mono<MAXV, false>(c, w, f.zt, L, d, hint, zdn, zup)
+                          : bracket_scan<MAXV, false>(c, w, f.zt, L, d, zdn, zup);
     if (layer < 0) return false;
     double x = d;
     x = dmax(zdn, dmin(x, zup));
@@ -398,13 +503,16 @@ __device__ __forceinline__ bool eval_stream(const Cell<MAXV>& c, int L, int V, c
 // reads it (TrajectoryCommon.h:176-185, quirk Q9), so it is unobservable.
 template <int MAXV>
 __device__ __forceinline__ bool eval_path(const Cell<MAXV>& c, int L, int V, const Field& ff, const Field& fb,
-                                          double px, double py, double pz, double d, double alpha, double& hx,
-                                          double& hy, double& hz, double& wv) {
+                                          double px, double py, double pz, double d, double alpha, int& hint0,
+                                          int& hint1, double& hx, double& hy, double& hz, double& wv) {
     double w[MAXV];
     if (!weights<MAXV>(c, L, V, px, py, pz, w)) return false;
     double zfdn, zfup, zbdn, zbup;
-    const int lf = bracket_scan<MAXV, true>(c, w, ff.zt, L, d, zfdn, zfup);
-    const int lb = bracket_scan<MAXV, true>(c, w, fb.zt, L, d, zbdn, zbup);
+    const bool wfin = weights_finite<MAXV>(c, w);
+    const int lf = (c.mono0 && wfin) ? bracket_mono<MAXV, true>(c, w, ff.zt, L, d, hint0, zfdn, zfup)
+                                   : bracket_scan<MAXV, true>(c, w, ff.zt, L, d, zfdn, zfup);
+    const int lb = (c.mono1 && wfin) ? bracket_mono<MAXV, true>(c, w, fb.zt, L, d, hint1, zbdn, zbup)
+                                   : bracket_scan<MAXV, true>(c, w, fb.zt, L, d, zbdn, zbup);
     if (lf < 0 || lb < 0) return false;
     const double xf = dmax(zfdn, dmin(d, zfup));
     const double denf = zfup - zfdn;
@@ -449,6 +557,9 @@ struct TrajArgs {
     const double4* __restrict__ vxyz;
     int C, V, L;
     dev::Field f0, f1;
+    const uint8_t* __restrict__ mono0;
+    const uint8_t* __restrict__ mono1;
+    const int* __restrict__ order;  // slot -> particle (NULL = identity)
     double* px; double* py; double* pz;
     float* depth;
     int* cell;
@@ -465,13 +576,19 @@ struct TrajArgs {
 
 template <int MAXV, bool PATH, bool EULER>
 __global__ void __launch_bounds__(kBlock) traj_kernel(TrajArgs a) {
-    const int64_t pid = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (pid >= a.n) return;
+    // XCD-aware mapping: blocks b, b+8, ... share an XCD (L2); give each XCD a
+    // contiguous range of the locality-ordered particles (bijective remap)
+    const unsigned nblk = gridDim.x, b = blockIdx.x, xcd = b % 8u, q = nblk / 8u, r = nblk % 8u;
+    const unsigned blk = (xcd < r ? xcd * (q + 1u) : r * (q + 1u) + (xcd - r) * q) + b / 8u;
+    const int64_t slot = (int64_t)blk * blockDim.x + threadIdx.x;
+    if (slot >= a.n) return;
+    const int64_t pid = a.order ? (int64_t)a.order[slot] : slot;
     if (a.death[pid] >= 0) return;  // the reference's lambda has returned
     double x = a.px[pid], y = a.py[pid], z = a.pz[pid];
     float dep = a.depth[pid];
     int cell = a.cell[pid];
     int died = -1;
+    int hint0 = -1, hint1 = -1;  // previous layer per field (speed only)
     dev::Cell<MAXV> c;
     c.id = -1;
     c.nv = 0;
@@ -479,14 +596,14 @@ __global__ void __launch_bounds__(kBlock) traj_kernel(TrajArgs a) {
     for (int64_t step = a.step_begin; step < a.step_end; ++step) {
         if (step == 0) {  // first_loop (:892-901)
             if (cell < 0 || cell >= C) { died = 0; break; }
-            dev::load_cell<MAXV>(c, cell, a.cellrec, a.vxyz);
+            dev::load_cell<MAXV>(c, cell, a.cellrec, a.vxyz, a.mono0, a.mono1);
             double* r0 = a.rec;
             r0[0 * a.rec_stride + pid] = x;
             r0[1 * a.rec_stride + pid] = y;
             r0[2 * a.rec_stride + pid] = z;
         } else {  // one-hop nearest-centre walk (:902-922)
             if (cell < 0 || cell >= C) { died = (int)step; break; }
-            if (c.id != cell) dev::load_cell<MAXV>(c, cell, a.cellrec, a.vxyz);
+            if (c.id != cell) dev::load_cell<MAXV>(c, cell, a.cellrec, a.vxyz, a.mono0, a.mono1);
             double best = 1.7976931348623157e308;
             int nc = cell;
 #pragma unroll
@@ -502,7 +619,7 @@ __global__ void __launch_bounds__(kBlock) traj_kernel(TrajArgs a) {
                 }
             }
             cell = nc;
-            if (c.id != cell) dev::load_cell<MAXV>(c, cell, a.cellrec, a.vxyz);
+            if (c.id != cell) dev::load_cell<MAXV>(c, cell, a.cellrec, a.vxyz, a.mono0, a.mono1);
         }
         const double d = -1.0 * (double)dep;
         const double r = dev::len3(x, y, z);
@@ -510,8 +627,8 @@ __global__ void __launch_bounds__(kBlock) traj_kernel(TrajArgs a) {
         double nx, ny, nz;
         const double alpha = PATH ? (double)step / (double)a.n_steps : 0.0;
         if (EULER) {
-            bool ok = PATH ? dev::eval_path<MAXV>(c, a.L, a.V, a.f0, a.f1, x, y, z, d, alpha, hx, hy, hz, wv)
-                           : dev::eval_stream<MAXV>(c, a.L, a.V, a.f0, x, y, z, d, hx, hy, hz, wv);
+            bool ok = PATH ? dev::eval_path<MAXV>(c, a.L, a.V, a.f0, a.f1, x, y, z, d, alpha, hint0, hint1, hx, hy, hz, wv)
+                           : dev::eval_stream<MAXV>(c, a.L, a.V, a.f0, x, y, z, d, hint0, hx, hy, hz, wv);
             if (!ok) { died = (int)step; break; }
             const double ax = y * hz - z * hy, ay = z * hx - x * hz, az = x * hy - y * hx;
             const double speed = dev::len3(hx, hy, hz);
@@ -522,22 +639,22 @@ __global__ void __launch_bounds__(kBlock) traj_kernel(TrajArgs a) {
             double s1x, s1y, s1z, s1w, s2x, s2y, s2z, s2w, s3x, s3y, s3z, s3w, s4x, s4y, s4z, s4w;
             double qx, qy, qz;
             const double a1 = alpha;
-            bool ok = PATH ? dev::eval_path<MAXV>(c, a.L, a.V, a.f0, a.f1, x, y, z, d, a1, s1x, s1y, s1z, s1w)
-                           : dev::eval_stream<MAXV>(c, a.L, a.V, a.f0, x, y, z, d, s1x, s1y, s1z, s1w);
+            bool ok = PATH ? dev::eval_path<MAXV>(c, a.L, a.V, a.f0, a.f1, x, y, z, d, a1, hint0, hint1, s1x, s1y, s1z, s1w)
+                           : dev::eval_stream<MAXV>(c, a.L, a.V, a.f0, x, y, z, d, hint0, s1x, s1y, s1z, s1w);
             if (!ok) { died = (int)step; break; }
             dev::advect(x, y, z, s1x, s1y, s1z, dt * 0.5, qx, qy, qz);
             const double a2 = PATH ? dev::dclamp(a1 + 0.5 * a.dalpha, 0.0, 1.0) : 0.0;
-            ok = PATH ? dev::eval_path<MAXV>(c, a.L, a.V, a.f0, a.f1, qx, qy, qz, d, a2, s2x, s2y, s2z, s2w)
-                      : dev::eval_stream<MAXV>(c, a.L, a.V, a.f0, qx, qy, qz, d, s2x, s2y, s2z, s2w);
+            ok = PATH ? dev::eval_path<MAXV>(c, a.L, a.V, a.f0, a.f1, qx, qy, qz, d, a2, hint0, hint1, s2x, s2y, s2z, s2w)
+                      : dev::eval_stream<MAXV>(c, a.L, a.V, a.f0, qx, qy, qz, d, hint0, s2x, s2y, s2z, s2w);
             if (!ok) { died = (int)step; break; }
             dev::advect(x, y, z, s2x, s2y, s2z, dt * 0.5, qx, qy, qz);
-            ok = PATH ? dev::eval_path<MAXV>(c, a.L, a.V, a.f0, a.f1, qx, qy, qz, d, a2, s3x, s3y, s3z, s3w)
-                      : dev::eval_stream<MAXV>(c, a.L, a.V, a.f0, qx, qy, qz, d, s3x, s3y, s3z, s3w);
+            ok = PATH ? dev::eval_path<MAXV>(c, a.L, a.V, a.f0, a.f1, qx, qy, qz, d, a2, hint0, hint1, s3x, s3y, s3z, s3w)
+                      : dev::eval_stream<MAXV>(c, a.L, a.V, a.f0, qx, qy, qz, d, hint0, s3x, s3y, s3z, s3w);
             if (!ok) { died = (int)step; break; }
             dev::advect(x, y, z, s3x, s3y, s3z, dt, qx, qy, qz);
             const double a4 = PATH ? dev::dclamp(a1 + a.dalpha, 0.0, 1.0) : 0.0;
-            ok = PATH ? dev::eval_path<MAXV>(c, a.L, a.V, a.f0, a.f1, qx, qy, qz, d, a4, s4x, s4y, s4z, s4w)
-                      : dev::eval_stream<MAXV>(c, a.L, a.V, a.f0, qx, qy, qz, d, s4x, s4y, s4z, s4w);
+            ok = PATH ? dev::eval_path<MAXV>(c, a.L, a.V, a.f0, a.f1, qx, qy, qz, d, a4, hint0, hint1, s4x, s4y, s4z, s4w)
+                      : dev::eval_stream<MAXV>(c, a.L, a.V, a.f0, qx, qy, qz, d, hint0, s4x, s4y, s4z, s4w);
             if (!ok) { died = (int)step; break; }
             // (s1 + 2 s2 + 2 s3 + s4) / 6 -- cy::Vec3 operator order (:959-960)
             hx = (((s1x + s2x * 2.0) + s3x * 2.0) + s4x) / 6.0;
@@ -799,6 +916,64 @@ __global__ void locate_kernel(int64_t n, const double* pts, int64_t C, const dou
 }
 
 // ===========================================================================
+// fast-path flags and particle locality order
+// ===========================================================================
+
+// d_mono[c] = 1 iff every vertex column of cell c is finite, |z| <= 1e6 m and
+// strictly decreasing by >= 1e-6 m per level (see bracket_mono).
+__global__ void mono_kernel(int64_t C, int maxv, int rec_ints, const int* cellrec, const double* zt, int L,
+                            uint8_t* mono) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= C) return;
+    const int* r = cellrec + i * rec_ints;
+    const int nv = r[0];
+    bool ok = (nv >= 1 && nv <= kMaxVertex && L >= 2);
+    for (int k = 0; k < nv && ok; ++k) {
+        const double* col = zt + (int64_t)r[1 + k] * L;
+        double prev = col[0];
+        ok = isfinite(prev) && fabs(prev) <= 1e6;
+        for (int l = 1; l < L && ok; ++l) {
+            const double z = col[l];
+            ok = isfinite(z) && fabs(z) <= 1e6 && (z < prev - 1e-6);
+            prev = z;
+        }
+    }
+    mono[i] = ok ? 1 : 0;
+}
+
+__device__ __forceinline__ uint64_t spread3(uint64_t v) {  // 21 bits -> every third bit
+    v &= 0x1fffffULL;
+    v = (v | (v << 32)) & 0x1f00000000ffffULL;
+    v = (v | (v << 16)) & 0x1f0000ff0000ffULL;
+    v = (v | (v << 8)) & 0x100f00f00f00f00fULL;
+    v = (v | (v << 4)) & 0x10c30c30c30c30c3ULL;
+    v = (v | (v << 2)) & 0x1249249249249249ULL;
+    return v;
+}
+
+__global__ void cell_key_kernel(int64_t C, const double4* cxyz, uint64_t* key) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= C) return;
+    const double4 p = cxyz[i];
+    const double r = sqrt(p.x * p.x + p.y * p.y + p.z * p.z);
+    const double s = (r > 0.0) ? 1.0 / r : 0.0;
+    const double m = 2097151.0;
+    const uint64_t qx = (uint64_t)fmin(fmax((p.x * s * 0.5 + 0.5) * m, 0.0), m);
+    const uint64_t qy = (uint64_t)fmin(fmax((p.y * s * 0.5 + 0.5) * m, 0.0), m);
+    const uint64_t qz = (uint64_t)fmin(fmax((p.z * s * 0.5 + 0.5) * m, 0.0), m);
+    key[i] = (spread3(qx) << 2) | (spread3(qy) << 1) | spread3(qz);
+}
+
+__global__ void particle_key_kernel(int64_t n, int64_t C, const int* cell, const uint64_t* cell_key, uint64_t* key,
+                                    int* idx) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const int c = cell[i];
+    key[i] = (c >= 0 && c < C) ? cell_key[c] : ~0ULL;
+    idx[i] = (int)i;
+}
+
+// ===========================================================================
 // host side
 // ===========================================================================
 namespace {
@@ -845,13 +1020,14 @@ mops_status upload(const T* h, size_t count, T** d, int64_t* acc, hipStream_t s)
 void free_mesh(mops_mesh* m) {
     if (!m) return;
     (void)hipFree(m->d_cellrec); (void)hipFree(m->d_cxyz); (void)hipFree(m->d_vxyz); (void)hipFree(m->d_cov);
-    (void)hipFree(m->d_bkeys); (void)hipFree(m->d_bcells);
+    (void)hipFree(m->d_bkeys); (void)hipFree(m->d_bcells); (void)hipFree(m->d_cell_key);
+    (void)hipFree(m->d_scratch);
     delete m;
 }
 
 void free_field(mops_field* f) {
     if (!f) return;
-    (void)hipFree(f->d_zt); (void)hipFree(f->d_vel); (void)hipFree(f->d_w);
+    (void)hipFree(f->d_zt); (void)hipFree(f->d_vel); (void)hipFree(f->d_w); (void)hipFree(f->d_mono);
     delete f;
 }
 
@@ -972,6 +1148,11 @@ mops_status mops_mesh_create(const mops_mesh_desc* desc, void* stream, mops_mesh
     if (e == hipSuccess) e = hipStreamSynchronize(s);
     (void)hipFree(tmp); (void)hipFree(keys_in); (void)hipFree(ids_in);
     if (e != hipSuccess) { free_mesh(m); return fail(MOPS_ERR_HIP, std::string("bucket sort: ") + hipGetErrorString(e)); }
+    if ((st = dmalloc(&m->d_cell_key, (size_t)C, &acc)) != MOPS_OK) { free_mesh(m); return st; }
+    cell_key_kernel<<<grid_for(C), kBlock, 0, s>>>(C, m->d_cxyz, m->d_cell_key);
+    e = hipGetLastError();
+    if (e == hipSuccess) e = hipStreamSynchronize(s);
+    if (e != hipSuccess) { free_mesh(m); return fail(MOPS_ERR_HIP, std::string("cell keys: ") + hipGetErrorString(e)); }
     m->bytes = acc;
     *out = m;
     return MOPS_OK;
@@ -979,6 +1160,14 @@ mops_status mops_mesh_create(const mops_mesh_desc* desc, void* stream, mops_mesh
 
 void mops_mesh_destroy(mops_mesh* mesh) { free_mesh(mesh); }
 int64_t mops_mesh_bytes(const mops_mesh* mesh) { return mesh ? mesh->bytes : 0; }
+
+static mops_status compute_mono(const mops_mesh* mesh, mops_field* f, hipStream_t s) {
+    MOPS_TRY(dmalloc(&f->d_mono, (size_t)mesh->C, &f->bytes));
+    mono_kernel<<<grid_for(mesh->C), kBlock, 0, s>>>(mesh->C, mesh->maxv, mesh->rec_ints, mesh->d_cellrec, f->d_zt,
+                                                    mesh->L, f->d_mono);
+    HIP_TRY(hipGetLastError());
+    return MOPS_OK;
+}
 
 mops_status mops_field_create_derived(const mops_mesh* mesh, const double* h_zt, const double* h_vel,
                                       const double* h_w, void* stream, mops_field** out) {
@@ -997,6 +1186,7 @@ mops_status mops_field_create_derived(const mops_mesh* mesh, const double* h_zt,
         if ((st = dmalloc(&f->d_w, V * (L + 1), &f->bytes)) != MOPS_OK) { free_field(f); return st; }
         HIP_TRY(hipMemsetAsync(f->d_w, 0, V * (L + 1) * sizeof(double), s));
     }
+    if ((st = compute_mono(mesh, f, s)) != MOPS_OK) { free_field(f); return st; }
     HIP_TRY(hipStreamSynchronize(s));
     *out = f;
     return MOPS_OK;
@@ -1050,6 +1240,7 @@ mops_status mops_field_create(const mops_mesh* mesh, const mops_snapshot_desc* d
         } else {
             (void)hipMemsetAsync(f->d_w, 0, (size_t)(V * (L + 1)) * sizeof(double), s);
         }
+        if ((st = compute_mono(mesh, f, s)) != MOPS_OK) break;
         hipError_t e = hipGetLastError();
         if (e == hipSuccess) e = hipStreamSynchronize(s);
         if (e != hipSuccess) { st = fail(MOPS_ERR_HIP, std::string("preprocessing: ") + hipGetErrorString(e)); break; }
@@ -1097,6 +1288,36 @@ mops_status mops_locate_cells(const mops_mesh* mesh, int64_t n, const double* d_
     return MOPS_OK;
 }
 
+mops_status mops_order_particles(const mops_mesh* mesh, int64_t n, const int32_t* d_cell, int32_t* d_order,
+                                 void* stream) {
+    if (!mesh || n < 0 || (n > 0 && (!d_cell || !d_order)) || n >= INT32_MAX)
+        return fail(MOPS_ERR_INVALID, "mops_order_particles: invalid argument");
+    if (n == 0) return MOPS_OK;
+    hipStream_t s = (hipStream_t)stream;
+    size_t tmp_bytes = 0;
+    HIP_TRY(hipcub::DeviceRadixSort::SortPairs(nullptr, tmp_bytes, (const uint64_t*)nullptr, (uint64_t*)nullptr,
+                                               (const int*)nullptr, (int*)nullptr, (int)n, 0, 64, s));
+    const size_t a8 = ((size_t)n * 8 + 255) / 256 * 256, a4 = ((size_t)n * 4 + 255) / 256 * 256;
+    const size_t need = 2 * a8 + a4 + tmp_bytes + 256;
+    if (mesh->scratch_bytes < need) {
+        HIP_TRY(hipStreamSynchronize(s));
+        (void)hipFree(mesh->d_scratch);
+        mesh->d_scratch = nullptr;
+        mesh->scratch_bytes = 0;
+        HIP_TRY(hipMalloc(&mesh->d_scratch, need));
+        mesh->scratch_bytes = need;
+    }
+    char* base = (char*)mesh->d_scratch;
+    uint64_t* kin = (uint64_t*)base;
+    uint64_t* kout = (uint64_t*)(base + a8);
+    int* vin = (int*)(base + 2 * a8);
+    void* tmp = base + 2 * a8 + a4;
+    particle_key_kernel<<<grid_for(n), kBlock, 0, s>>>(n, mesh->C, d_cell, mesh->d_cell_key, kin, vin);
+    HIP_TRY(hipGetLastError());
+    HIP_TRY(hipcub::DeviceRadixSort::SortPairs(tmp, tmp_bytes, kin, kout, vin, d_order, (int)n, 0, 64, s));
+    return MOPS_OK;
+}
+
 int64_t mops_traj_num_records(const mops_traj_cfg* cfg) {
     if (!cfg || cfg->record_t <= 0) return 0;
     return cfg->simulation_duration / cfg->record_t;
@@ -1129,6 +1350,9 @@ mops_status mops_traj_advance(const mops_mesh* mesh, const mops_field* front, co
     a.C = (int)mesh->C; a.V = (int)mesh->V; a.L = mesh->L;
     a.f0 = dev::Field{front->d_zt, front->d_vel, front->d_w};
     a.f1 = back ? dev::Field{back->d_zt, back->d_vel, back->d_w} : a.f0;
+    a.mono0 = front->d_mono;
+    a.mono1 = back ? back->d_mono : front->d_mono;
+    a.order = p->d_order;
     a.px = p->d_x; a.py = p->d_y; a.pz = p->d_z; a.depth = p->d_depth; a.cell = p->d_cell; a.death = p->d_death_step;
     a.n = p->n;
     a.step_begin = step_begin; a.step_end = step_end; a.n_steps = n_steps;
@@ -1195,7 +1419,7 @@ mops_status mops_run_trajectories(const mops_mesh* mesh, const mops_field* front
     double *seeds = nullptr, *x = nullptr, *y = nullptr, *z = nullptr, *rec = nullptr;
     double *pts = nullptr, *vel = nullptr, *tmp = nullptr, *sal = nullptr, *last = nullptr;
     float* dep = nullptr;
-    int *cells = nullptr, *death = nullptr;
+    int *cells = nullptr, *death = nullptr, *order = nullptr;
     mops_status st = MOPS_OK;
     std::vector<double> hx((size_t)n), hy((size_t)n), hz((size_t)n);
     std::vector<float> hd((size_t)n);
@@ -1206,6 +1430,7 @@ mops_status mops_run_trajectories(const mops_mesh* mesh, const mops_field* front
     auto cleanup = [&]() {
         (void)hipFree(seeds); (void)hipFree(x); (void)hipFree(y); (void)hipFree(z); (void)hipFree(rec); (void)hipFree(pts); (void)hipFree(vel);
         (void)hipFree(tmp); (void)hipFree(sal); (void)hipFree(last); (void)hipFree(dep); (void)hipFree(cells); (void)hipFree(death);
+        (void)hipFree(order);
     };
     do {
         if ((st = upload(h_seeds, (size_t)(3 * n), &seeds, nullptr, s)) != MOPS_OK) break;
@@ -1247,7 +1472,9 @@ mops_status mops_run_trajectories(const mops_mesh* mesh, const mops_field* front
         }
         e = hipMemcpyAsync(cells, hc.data(), (size_t)n * sizeof(int32_t), hipMemcpyHostToDevice, s);
         if (e != hipSuccess) { st = fail(MOPS_ERR_HIP, hipGetErrorString(e)); break; }
-        mops_particles prt{n, x, y, z, dep, cells, death};
+        if ((st = dmalloc(&order, (size_t)n, nullptr)) != MOPS_OK) break;
+        if ((st = mops_order_particles(mesh, n, cells, order, stream)) != MOPS_OK) break;
+        mops_particles prt{n, x, y, z, dep, cells, death, order};
         if ((st = mops_traj_advance(mesh, front, back, cfg, &prt, 0, n_steps, rec, n, stream)) != MOPS_OK) break;
         if ((st = mops_traj_finalize(n, K, seeds, rec, n, back ? 1 : 0, pts, vel, tmp, sal, last, stream)) != MOPS_OK)
             break;

@@ -193,8 +193,9 @@ class ParticleSet:
     """
 
     def __init__(self, mesh: DeviceMesh, seeds_xyz, depth: float | np.ndarray, cfg: TrajectoryConfig, device=None,
-                 cells=None):
+                 cells=None, use_order: bool = True):
         import torch
+        self.use_order = use_order
         self.torch = torch
         dev = device or torch.device("cuda", torch.cuda.current_device())
         s = torch.as_tensor(np.ascontiguousarray(seeds_xyz, dtype=np.float64).reshape(-1, 3), device=dev)
@@ -216,7 +217,15 @@ class ParticleSet:
             self.cell = torch.as_tensor(np.asarray(cells, dtype=np.int32), device=dev).contiguous()
         self.K = cfg.n_records
         self.records = torch.zeros((max(self.K, 1), 6, self.n), dtype=torch.float64, device=dev)
+        self.order = torch.empty((self.n,), dtype=torch.int32, device=dev)
         self._c = cfg.ctype()
+        self.reorder(stream=torch.cuda.current_stream(dev).cuda_stream)
+
+    def reorder(self, stream=None):
+        """Locality order of the particles by their current cell (mops_order_particles)."""
+        L.check(L.load().mops_order_particles(self.mesh.handle, self.n, C.c_void_p(self.cell.data_ptr()),
+                                              C.c_void_p(self.order.data_ptr()), _stream_handle(stream)),
+                "mops_order_particles")
 
     def reset(self, seeds_xyz=None, depth=None):
         if seeds_xyz is not None:
@@ -229,7 +238,8 @@ class ParticleSet:
 
     def particles(self) -> L.Particles:
         return L.Particles(self.n, self.x.data_ptr(), self.y.data_ptr(), self.z.data_ptr(), self.depth.data_ptr(),
-                           self.cell.data_ptr(), self.death.data_ptr())
+                           self.cell.data_ptr(), self.death.data_ptr(),
+                           self.order.data_ptr() if self.use_order else None)
 
     def advance(self, front: DeviceField, back: DeviceField | None, step_begin: int, step_end: int, stream=None):
         p = self.particles()

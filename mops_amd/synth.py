@@ -252,7 +252,8 @@ class Snapshot:
 
 
 def make_snapshot(mesh: Mesh, timestep: int = 0, phase: float = 0.0, u0: float = 0.5,
-                  u1: float = 0.25, w0: float = 1.0e-5, land_zero: bool = True) -> Snapshot:
+                  u1: float = 0.25, w0: float = 1.0e-5, land_zero: bool = True,
+                  inversions: float = 0.0, inversion_seed: int = 3) -> Snapshot:
     """Solid-body flow + a travelling wave-3 perturbation, decaying with depth.
 
     ``phase`` (radians) shifts the perturbation eastward so consecutive daily
@@ -267,6 +268,16 @@ def make_snapshot(mesh: Mesh, timestep: int = 0, phase: float = 0.0, u0: float =
     ref_dz = np.diff(np.concatenate([[0.0], mesh.refBottomDepth]))
     ssh = 0.5 * np.cos(lat) * np.sin(2.0 * lon + phase)
     thick = ref_dz[None, :] * ((bot + ssh) / H)[:, None]
+    if inversions > 0.0:
+        # negative / zero layer thicknesses in a fraction of cells: the zTop
+        # column is then non-monotone and the reference's fix-up (and the
+        # engine's general bracket path) is exercised
+        rng = np.random.default_rng(inversion_seed)
+        sel = rng.random(C) < inversions
+        lv = rng.integers(1, L - 1, size=C)
+        rows = np.nonzero(sel)[0]
+        thick[rows, lv[rows]] *= -0.5
+        thick[rows, np.minimum(lv[rows] + 1, L - 1)] = 0.0
     # mid-layer depth (positive down) for the decay profile
     zmid = np.cumsum(thick, axis=1) - 0.5 * thick
     decay = np.exp(-zmid / 1500.0)

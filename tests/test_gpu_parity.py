@@ -185,3 +185,46 @@ def test_medium_mesh_l60_parity(gpu, engine_lib, medium_case, oracle_lib):
         ref = oracle_lib.run(mesh, r0, None, seeds, depths=depths, delta_t=120, duration=43200, record_t=3600,
                              euler=(method == 1), cells=got["cells"])
         assert_lines_match(got, ref, f"medium method={method}")
+
+
+@pytest.mark.parametrize("method", ["euler", "rk4"])
+def test_nonmonotone_columns(gpu, engine_lib, small_case, oracle_lib, method):
+    """Inverted / zero-thickness layers: the reference's monotone fix-up fires
+    and the engine must take its general (streaming) bracket path."""
+    from mops_amd import synth
+    from mops_amd.engine import DeviceField, DeviceMesh, TrajectoryConfig, run_trajectories
+    mesh, _, _ = small_case
+    s0 = synth.make_snapshot(mesh, timestep=0, inversions=0.4)
+    s1 = synth.make_snapshot(mesh, timestep=1, phase=0.35, inversions=0.4, inversion_seed=4)
+    dm = DeviceMesh.from_mesh(mesh)
+    f0, f1 = DeviceField.from_snapshot(dm, s0), DeviceField.from_snapshot(dm, s1)
+    r0, r1 = oracle_lib.preprocess(mesh, s0), oracle_lib.preprocess(mesh, s1)
+    zt, _, _ = f0.export()
+    assert np.array_equal(zt, r0.vertex_ztop)
+    seeds = synth.uniform_band_seeds(600, seed=31)
+    rng = np.random.default_rng(2)
+    depths = rng.uniform(0.0, 3000.0, len(seeds)).astype(np.float32)
+    for back, rb in ((None, None), (f1, r1)):
+        cfg = TrajectoryConfig(deltaT=120, simulationDuration=43200, recordT=3600, depth=0.0,
+                               method=1 if method == "euler" else 0)
+        got = run_trajectories(dm, f0, back, cfg, seeds, depths=depths)
+        ref = oracle_lib.run(mesh, r0, rb, seeds, depths=depths, delta_t=120, duration=43200, record_t=3600,
+                             euler=(method == "euler"), cells=got["cells"])
+        assert_lines_match(got, ref, f"nonmonotone {method} path={back is not None}")
+
+
+def test_order_is_permutation_and_result_invariant(gpu, dev_small, small_case):
+    import torch
+    from mops_amd import synth
+    from mops_amd.engine import ParticleSet, TrajectoryConfig
+    dm, f0, f1 = dev_small
+    seeds = synth.uniform_band_seeds(3000, seed=77)
+    cfg = TrajectoryConfig(deltaT=120, simulationDuration=21600, recordT=3600, depth=300.0, method=0)
+    a = ParticleSet(dm, seeds, 300.0, cfg, use_order=True)
+    b = ParticleSet(dm, seeds, 300.0, cfg, use_order=False)
+    order = a.order.cpu().numpy()
+    assert np.array_equal(np.sort(order), np.arange(len(seeds)))
+    for ps in (a, b):
+        ps.advance(f0, f1, 0, cfg.n_steps)
+    torch.cuda.synchronize()
+    assert torch.equal(a.records, b.records) and torch.equal(a.death, b.death)
