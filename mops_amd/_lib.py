@@ -64,7 +64,7 @@ def load(path: str | None = None):
     global _lib
     if _lib is not None:
         return _lib
-    path = path or LIB_PATH
+    path = path or os.environ.get("MOPS_TRAJ_LIB") or LIB_PATH
     if not os.path.exists(path):
         raise MopsError(f"HIP engine library not found at {path}: run `python -c \"import __graft_entry__ as g; "
                         f"g.build()\"` (hipcc --offload-arch=gfx950) first")

@@ -574,8 +574,17 @@ struct TrajArgs {
     int64_t rec_stride;
 };
 
+#ifndef MOPS_TRAJ_WAVES_PER_EU
+#define MOPS_TRAJ_WAVES_PER_EU 0
+#endif
+#if MOPS_TRAJ_WAVES_PER_EU > 0
+#define MOPS_TRAJ_BOUNDS __launch_bounds__(kBlock, MOPS_TRAJ_WAVES_PER_EU)
+#else
+#define MOPS_TRAJ_BOUNDS __launch_bounds__(kBlock)
+#endif
+
 template <int MAXV, bool PATH, bool EULER>
-__global__ void __launch_bounds__(kBlock) traj_kernel(TrajArgs a) {
+__global__ void MOPS_TRAJ_BOUNDS traj_kernel(TrajArgs a) {
     // XCD-aware mapping: blocks b, b+8, ... share an XCD (L2); give each XCD a
     // contiguous range of the locality-ordered particles (bijective remap)
     const unsigned nblk = gridDim.x, b = blockIdx.x, xcd = b % 8u, q = nblk / 8u, r = nblk % 8u;

@@ -1,0 +1,184 @@
+"""CPU-side tests: synthetic meshes, the C ABI library surface (no GPU
+compute), host logic, and the multi-rank sharding with gloo."""
+import os
+import re
+
+import numpy as np
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+# ---------------------------------------------------------------- meshes
+@pytest.mark.parametrize("land", ["none", "continents"])
+def test_mesh_is_valid_mpas_layout(land):
+    from mops_amd import synth
+    m = synth.make_mesh(12, n_levels=5, land=land)
+    C, mE = m.nCells, m.maxEdges
+    voc = m.verticesOnCell.reshape(C, mE).astype(np.int64) - 1
+    coc = m.cellsOnCell.reshape(C, mE).astype(np.int64) - 1
+    ne = m.nEdgesOnCell.astype(int)
+    assert m.nVertices == m.cellsOnVertex.size // 3
+    for c in range(C):
+        p = m.cellCoord[c]
+        for k in range(ne[c]):
+            a, b = m.vertexCoord[voc[c, k]], m.vertexCoord[voc[c, (k + 1) % ne[c]]]
+            assert np.dot(np.cross(a, b), p) > 0           # CCW, centre inside (IsInMesh)
+            d = coc[c, k]
+            if d >= 0:
+                assert c in coc[d, : ne[d]]                # symmetric neighbours
+        assert np.all(voc[c, ne[c]:] == -1)                # zero padding
+    if land == "none":
+        assert C == 10 * 12 ** 2 + 2 and np.all(coc[np.arange(mE)[None, :] < ne[:, None]] >= 0)
+    else:
+        assert (m.cellsOnVertex == 0).any()                # culled coast
+
+
+def test_frequency_for_cells():
+    from mops_amd import synth
+    assert synth.frequency_for_cells(236000) in (153, 154)
+
+
+# ---------------------------------------------------------------- C ABI
+def _header_functions():
+    src = open(os.path.join(ROOT, "include", "mops_traj.h")).read()
+    src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
+    return sorted(set(re.findall(r"\b(mops_[a-z_0-9]+)\s*\(", src)))
+
+
+def test_abi_exports_every_header_symbol(engine_lib):
+    from mops_amd import _lib
+    names = _header_functions()
+    assert set(names) == set(_lib.EXPORTED)
+    for n in names:
+        assert hasattr(engine_lib, n), n
+
+
+def test_abi_host_only_calls(engine_lib):
+    import ctypes as C
+    from mops_amd import _lib
+    assert engine_lib.mops_abi_version() == 1
+    cfg = _lib.TrajCfg(120, 86400, 3600, 0, 1)
+    assert engine_lib.mops_traj_num_records(C.byref(cfg)) == 24
+    assert engine_lib.mops_traj_num_steps(C.byref(cfg)) == 720
+    # invalid settings are rejected before any device work (reference: Error() + {})
+    bad = _lib.TrajCfg(0, 86400, 3600, 0, 1)
+    p = _lib.Particles(0, None, None, None, None, None, None, None)
+    st = engine_lib.mops_traj_advance(None, None, None, C.byref(bad), C.byref(p), 0, 1, None, 0, None)
+    assert st == _lib.MOPS_ERR_INVALID
+    assert b"invalid" in engine_lib.mops_last_error()
+    h = C.c_void_p()
+    desc = _lib.MeshDesc(0, 0, 7, 60, None, None, None, None, None, None)
+    assert engine_lib.mops_mesh_create(C.byref(desc), None, C.byref(h)) == _lib.MOPS_ERR_INVALID
+    desc = _lib.MeshDesc(10, 10, 21, 60, None, None, None, None, None, None)
+    assert engine_lib.mops_mesh_create(C.byref(desc), None, C.byref(h)) == _lib.MOPS_ERR_UNSUPPORTED
+
+
+def test_library_missing_fails_loudly(tmp_path):
+    from mops_amd import _lib
+    with pytest.raises(_lib.MopsError):
+        saved = _lib._lib
+        try:
+            _lib._lib = None
+            _lib.load(str(tmp_path / "nope.so"))
+        finally:
+            _lib._lib = saved
+
+
+def test_oracle_not_imported_by_product():
+    """The product package never references the oracle (test infrastructure)."""
+    pkg = os.path.join(ROOT, "mops_amd")
+    for dirpath, _, files in os.walk(pkg):
+        for f in files:
+            if f.endswith((".py", ".hip", ".cpp", ".h")):
+                txt = open(os.path.join(dirpath, f)).read()
+                assert "import oracle" not in txt and "from oracle" not in txt, f
+                assert "mops_oracle" not in txt and "orc_" not in txt, f
+
+
+# ---------------------------------------------------------------- host logic
+def test_shard_bounds_cover_exactly():
+    from mops_amd.distributed import max_shard, shard_bounds
+    for n in (0, 1, 7, 100, 1001):
+        for w in (1, 2, 3, 8):
+            spans = [shard_bounds(n, r, w) for r in range(w)]
+            assert spans[0][0] == 0 and spans[-1][1] == n
+            assert all(spans[i][1] == spans[i + 1][0] for i in range(w - 1))
+            assert max(h - l for l, h in spans) == max_shard(n, w) or n == 0
+
+
+def test_record_period_rules():
+    import math
+    from mops_amd.engine import TrajectoryConfig
+    # streamline: run_time % recordT == 0, run_time = (j+1)*dt
+    for dt, rt in ((120, 3600), (120, 300), (60, 90), (7, 3600)):
+        per = rt // math.gcd(rt, dt)
+        steps = [j for j in range(20000) if ((j + 1) * dt) % rt == 0]
+        assert steps[:5] == [per * (i + 1) - 1 for i in range(5)]
+    cfg = TrajectoryConfig(deltaT=60, simulationDuration=7 * 86400, recordT=3600)
+    assert cfg.n_steps == 10080 and cfg.n_records == 168
+
+
+def test_bench_bytes_model():
+    import importlib.util
+    spec = importlib.util.spec_from_file_location("bench", os.path.join(ROOT, "bench.py"))
+    bench = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(bench)
+    # nv = 6 -> 3.66 kB (streamline L=60), 6.9 kB (pathline L=60), 8.8 kB (L=80)
+    assert abs(bench.algorithmic_bytes_per_pstep(6, 60, 1) - 3660) < 5
+    assert abs(bench.algorithmic_bytes_per_pstep(6, 60, 2) - 6924) < 50
+    assert abs(bench.algorithmic_bytes_per_pstep(6, 80, 2) - 8844) < 50
+
+
+# ---------------------------------------------------------------- gloo, world_size 2
+def _gloo_worker(rank, world, port, q):
+    import torch.distributed as dist
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        import torch
+        from mops_amd import synth
+        from mops_amd.distributed import max_shard, shard_bounds, unshard
+        from oracle import oracle as O
+        mesh = synth.make_mesh(10, n_levels=8)
+        s0 = synth.make_snapshot(mesh)
+        d0 = O.preprocess(mesh, s0)
+        seeds = synth.uniform_band_seeds(101, seed=9)
+        lo, hi = shard_bounds(len(seeds), rank, world)
+        npad = max_shard(len(seeds), world)
+        r = O.run(mesh, d0, None, seeds[lo:hi], depth=200.0, delta_t=300, duration=10800, record_t=3600,
+                  n_threads=1, finalize=False)
+        K = r["rec_pos"].shape[1]
+        slab = torch.zeros((K, 6, npad), dtype=torch.float64)
+        slab[:, :3, : hi - lo] = torch.as_tensor(r["rec_pos"].transpose(1, 2, 0))
+        slab[:, 3:, : hi - lo] = torch.as_tensor(r["rec_vel"].transpose(1, 2, 0))
+        out = [torch.empty_like(slab) for _ in range(world)]
+        dist.all_gather(out, slab)       # gloo has no all_gather_into_tensor on CPU for all versions
+        full = unshard(torch.stack(out), len(seeds), world)
+        if rank == 0:
+            ref = O.run(mesh, d0, None, seeds, depth=200.0, delta_t=300, duration=10800, record_t=3600,
+                        n_threads=1, finalize=False)
+            ok = (np.array_equal(full[:, :3].numpy().transpose(2, 0, 1), ref["rec_pos"]) and
+                  np.array_equal(full[:, 3:].numpy().transpose(2, 0, 1), ref["rec_vel"]))
+            q.put(bool(ok))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_sharded_records_gloo_world2():
+    import multiprocessing as mp
+    import socket
+    from oracle import oracle as O
+    O.build()
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    procs = [ctx.Process(target=_gloo_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    for p in procs:
+        p.join(timeout=240)
+    assert all(p.exitcode == 0 for p in procs)
+    assert q.get(timeout=5) is True
