@@ -91,6 +91,11 @@ struct mops_field {
     double* d_vel = nullptr;  // cellVertexVelocity [V][L][3]
     double* d_w = nullptr;    // cellVertexVertVelocity [V][L+1]
     uint8_t* d_mono = nullptr;  // [C] 1 = every vertex column of the cell strictly decreasing (margin)
+    // level-pair records [V][L-1][12] doubles, record k-1 of vertex v =
+    // {z_0, z_{k-1}, z_k, w_{k-1}, w_k, vel_{k-1} (3), vel_k (3), pad}: one
+    // 96-B, 16-B-aligned read gives a vertex's whole contribution when the
+    // particle sits in layer k
+    double* d_pr = nullptr;
     int64_t bytes = 0;
 };
 
@@ -144,8 +149,9 @@ struct Cell {
     int id;
     int nv;
     bool mono0, mono1;  // fast-path flags of the cell for the front / back field
+    double cx, cy, cz;  // cell centre
+    double rs2;         // squared "stay" radius (see traj_kernel's walk)
     int vid[MAXV];
-    int coc[MAXV];
     double x[MAXV], y[MAXV], z[MAXV];
     double B[MAXV];  // Wachspress B_i = area(poly[i-1], poly[i], poly[i+1]) (depends on the polygon only)
 };
@@ -153,9 +159,13 @@ struct Cell {
 template <int MAXV>
 __device__ __forceinline__ void load_cell(Cell<MAXV>& c, int cell, const int* __restrict__ cellrec,
                                           const double4* __restrict__ vxyz, const uint8_t* __restrict__ mono0,
-                                          const uint8_t* __restrict__ mono1) {
+                                          const uint8_t* __restrict__ mono1, const double4* __restrict__ cxyz) {
     c.mono0 = mono0[cell] != 0;
     c.mono1 = mono1[cell] != 0;
+    {
+        const double4 q = cxyz[cell];
+        c.cx = q.x; c.cy = q.y; c.cz = q.z; c.rs2 = q.w;
+    }
     constexpr int REC = ((1 + 2 * MAXV) + 3) / 4 * 4;
     const int* r = cellrec + (int64_t)cell * REC;
     int buf[REC];
@@ -170,7 +180,6 @@ __device__ __forceinline__ void load_cell(Cell<MAXV>& c, int cell, const int* __
 #pragma unroll
     for (int k = 0; k < MAXV; ++k) {
         c.vid[k] = buf[1 + k];
-        c.coc[k] = buf[1 + MAXV + k];
         if (k < nv) {
             const double4 p = vxyz[c.vid[k]];
             c.x[k] = p.x; c.y[k] = p.y; c.z[k] = p.z;
@@ -352,27 +361,43 @@ template <int MAXV, bool PATH>
 __device__ __forceinline__ int bracket_mono(const Cell<MAXV>& c, const double* w, const double* __restrict__ zt,
                                             int L, double d, int& hint, double& zdn, double& zup) {
     const double eps = 1e-8;
-    const double z0 = col<MAXV>(c, w, zt, L, 0);
+    int h = hint;
+    const bool hint_ok = (h >= 1 && h <= L - 1);
+    if (!hint_ok) h = 1;
+    // one batch of independent loads: z_0, z_{h-1}, z_h (per-level sums keep
+    // the reference's vertex order)
+    double z0 = 0.0, zhm1 = 0.0, zh = 0.0;
+#pragma unroll
+    for (int v = 0; v < MAXV; ++v) {
+        if (v < c.nv) {
+            const double* q = zt + (int64_t)c.vid[v] * L;
+            const double q0 = q[0], q1 = q[h - 1], q2 = q[h];
+            z0 += w[v] * q0;
+            zhm1 += w[v] * q1;
+            zh += w[v] * q2;
+        }
+    }
     if (d > z0 + eps) {  // above the surface (PATH: see DESIGN.md Q4)
-        zdn = col<MAXV>(c, w, zt, L, 1); zup = z0; hint = 1;
+        zdn = (h == 1) ? zh : ((h == 2) ? zhm1 : col<MAXV>(c, w, zt, L, 1));
+        zup = z0; hint = 1;
         return 1;
     }
-    int h = hint;
-    if (h < 1 || h > L - 1) {  // no hint: lower_bound of Q over [1, L-1] by bisection
+    if (!hint_ok) {  // no hint: lower_bound of Q over [1, L-1] by bisection
         int lo = 1, hi = L;
         while (lo < hi) {
             const int mid = (lo + hi) >> 1;
             if (d >= col<MAXV>(c, w, zt, L, mid) - eps) hi = mid; else lo = mid + 1;
         }
         h = (lo <= L - 1) ? lo : L - 1;
+        zh = col<MAXV>(c, w, zt, L, h);
+        zhm1 = (h == 1) ? z0 : col<MAXV>(c, w, zt, L, h - 1);
     }
     int a;
     double za, zam1;  // z_a, z_{a-1}
-    const double zh = col<MAXV>(c, w, zt, L, h);
     if (d >= zh - eps) {  // a <= h: walk towards the surface
         int k = h;
         double zk = zh;
-        double zkm1 = (k == 1) ? z0 : col<MAXV>(c, w, zt, L, k - 1);
+        double zkm1 = zhm1;
         while (k > 1 && d >= zkm1 - eps) {
             --k;
             zk = zkm1;
@@ -390,7 +415,7 @@ __device__ __forceinline__ int bracket_mono(const Cell<MAXV>& c, const double* w
             if (d >= zk - eps) { found = true; break; }
         }
         if (!found) {  // Q(L-1) false  <=>  d < z_{L-1} - eps: the "below the bottom" branch
-            const double zlm1 = (k == h) ? ((L - 2 == 0) ? z0 : col<MAXV>(c, w, zt, L, L - 2)) : zprev;
+            const double zlm1 = (k == h) ? zhm1 : zprev;
             zdn = zk; zup = zlm1; hint = L - 1;
             return L - 1;
         }
@@ -432,36 +457,78 @@ __device__ __forceinline__ bool weights_finite(const Cell<MAXV>& c, const double
     return ok;
 }
 
+struct Field {
+    const double* __restrict__ zt;   // cellVertexZTop [V][L]
+    const double* __restrict__ pr;   // level-pair records [V][L-1][12] (see mops_field)
+};
+
+// Weighted sums of one level-pair record per vertex: everything an
+// evaluation needs when the particle's layer is k.  Each sum keeps the
+// reference's vertex order, so every value equals its reference counterpart
+// (col(), TBBKernel::CalcVelocity, CalcAttribute) bit for bit.
+struct Pair {
+    double z0, zm, zk;   // z_0, z_{k-1}, z_k
+    double wm, wk;       // vertical velocity at interfaces k-1, k
+    double um0, um1, um2, uk0, uk1, uk2;  // horizontal velocity at levels k-1, k
+};
+
 template <int MAXV>
-__device__ __forceinline__ void vel_at(const Cell<MAXV>& c, const double* w, const double* __restrict__ vel, int L,
-                                       int layer, double& vx, double& vy, double& vz) {
-    vx = 0.0; vy = 0.0; vz = 0.0;
+__device__ __forceinline__ void pair_sums(const Cell<MAXV>& c, const double* w, const double* __restrict__ pr, int L,
+                                          int k, Pair& S) {
+    S.z0 = S.zm = S.zk = S.wm = S.wk = 0.0;
+    S.um0 = S.um1 = S.um2 = S.uk0 = S.uk1 = S.uk2 = 0.0;
 #pragma unroll
     for (int v = 0; v < MAXV; ++v) {
         if (v < c.nv) {
-            const double* q = vel + ((int64_t)c.vid[v] * L + layer) * 3;
-            vx += w[v] * q[0];
-            vy += w[v] * q[1];
-            vz += w[v] * q[2];
+            const double2* r = reinterpret_cast<const double2*>(pr + ((int64_t)c.vid[v] * (L - 1) + (k - 1)) * 12);
+            const double2 a0 = r[0], a1 = r[1], a2 = r[2], a3 = r[3], a4 = r[4], a5 = r[5];
+            const double wv = w[v];
+            S.z0 += wv * a0.x; S.zm += wv * a0.y; S.zk += wv * a1.x;
+            S.wm += wv * a1.y; S.wk += wv * a2.x;
+            S.um0 += wv * a2.y; S.um1 += wv * a3.x; S.um2 += wv * a3.y;
+            S.uk0 += wv * a4.x; S.uk1 += wv * a4.y; S.uk2 += wv * a5.x;
         }
     }
 }
 
-template <int MAXV>
-__device__ __forceinline__ double attr_at(const Cell<MAXV>& c, const double* w, const double* __restrict__ a, int Lt,
-                                          int layer) {
-    double r = 0.0;
-#pragma unroll
-    for (int v = 0; v < MAXV; ++v)
-        if (v < c.nv) r += w[v] * a[(int64_t)c.vid[v] * Lt + layer];
-    return r;
+// Layer + values for one field.  Fast path (monotone cell, finite weights,
+// valid hint h): ONE record per vertex decides whether the layer is h --
+// surface test on z_0, then Q(h), !Q(h-1), !P(h+1) (notation of
+// bracket_scan), i.e. a = b = h, which both the binary search (streamline)
+// and the linear scan (pathline) resolve to h.  Otherwise the exact general
+// bracket runs and the record of the final layer is read.
+template <int MAXV, bool PATH>
+__device__ __forceinline__ int layer_eval(const Cell<MAXV>& c, const double* w, bool mono_ok, const Field& f, int L,
+                                          double d, int& hint, Pair& S) {
+    const double eps = 1e-8;
+    const int h = hint;
+    if (mono_ok && h >= 1 && h <= L - 1) {
+        pair_sums<MAXV>(c, w, f.pr, L, h, S);
+        bool ok;
+        if (d > S.z0 + eps) {
+            ok = (h == 1);
+        } else {
+            const bool Qh = d >= S.zk - eps;
+            const bool Qm = (h > 1) && (d >= S.zm - eps);
+            const bool Pn = (h < L - 1) && (d <= S.zk + eps);
+            ok = Qh && !Qm && !Pn;
+        }
+        if (ok) return h;
+    }
+    double zdn, zup;
+    int layer;
+    if (mono_ok) {
+        layer = bracket_mono<MAXV, PATH>(c, w, f.zt, L, d, hint, zdn, zup);
+    } else {
+        layer = bracket_scan<MAXV, PATH>(c, w, f.zt, L, d, zdn, zup);
+        hint = layer;
+    }
+    if (layer < 0) return -1;
+    pair_sums<MAXV>(c, w, f.pr, L, layer, S);
+    S.zk = zdn;  // the bracket's (possibly fixed-up) column values
+    S.zm = zup;
+    return layer;
 }
-
-struct Field {
-    const double* __restrict__ zt;
-    const double* __restrict__ vel;
-    const double* __restrict__ w;
-};
 
 // streamline calc_velocity_at (MPASOVisualizerKernels.cpp:740-872)
 template <int MAXV>
@@ -470,31 +537,22 @@ __device__ __forceinline__ bool eval_stream(const Cell<MAXV>& c, int L, int V, c
                                             double& wv) {
     double w[MAXV];
     if (!weights<MAXV>(c, L, V, px, py, pz, w)) return false;
-    double zdn, zup;
-    const int layer = (c.mono0 && weights_finite<MAXV>(c, w))
-                          ? bracket_mono<MAXV, false>(c, w, f.zt, L, d, hint, zdn, zup)
-                          : bracket_scan<MAXV, false>(c, w, f.zt, L, d, zdn, zup);
+    Pair S;
+    const int layer = layer_eval<MAXV, false>(c, w, c.mono0 && weights_finite<MAXV>(c, w), f, L, d, hint, S);
     if (layer < 0) return false;
+    const double zdn = S.zk, zup = S.zm;
     double x = d;
     x = dmax(zdn, dmin(x, zup));
     const double den = zup - zdn;
     if (fabs(den) < 1e-12) return false;
     const double t = (x - zdn) / den;
-    double dx, dy, dz, ux, uy, uz;
-    vel_at<MAXV>(c, w, f.vel, L, layer, dx, dy, dz);
-    vel_at<MAXV>(c, w, f.vel, L, layer - 1, ux, uy, uz);
-    if (len3(dx, dy, dz) < 1e-12 || len3(ux, uy, uz) < 1e-12) return false;
-    hx = ux * t + dx * (1.0 - t);
-    hy = uy * t + dy * (1.0 - t);
-    hz = uz * t + dz * (1.0 - t);
+    // vel_dn at `layer`, vel_up at `layer - 1`; w at interfaces layer, layer-1
+    if (len3(S.uk0, S.uk1, S.uk2) < 1e-12 || len3(S.um0, S.um1, S.um2) < 1e-12) return false;
+    hx = S.um0 * t + S.uk0 * (1.0 - t);
+    hy = S.um1 * t + S.uk1 * (1.0 - t);
+    hz = S.um2 * t + S.uk2 * (1.0 - t);
     if (len3(hx, hy, hz) < 1e-12) return false;
-    const int Lp1 = L + 1;
-    int dn_if = layer, up_if = (layer > 0) ? (layer - 1) : 0;
-    if (dn_if >= Lp1) dn_if = Lp1 - 1;
-    if (up_if >= Lp1) up_if = Lp1 - 1;
-    const double wdn = attr_at<MAXV>(c, w, f.w, Lp1, dn_if);
-    const double wup = attr_at<MAXV>(c, w, f.w, Lp1, up_if);
-    wv = t * wup + (1.0 - t) * wdn;
+    wv = t * S.wm + (1.0 - t) * S.wk;
     return true;
 }
 
@@ -507,41 +565,28 @@ __device__ __forceinline__ bool eval_path(const Cell<MAXV>& c, int L, int V, con
                                           int& hint1, double& hx, double& hy, double& hz, double& wv) {
     double w[MAXV];
     if (!weights<MAXV>(c, L, V, px, py, pz, w)) return false;
-    double zfdn, zfup, zbdn, zbup;
     const bool wfin = weights_finite<MAXV>(c, w);
-    const int lf = (c.mono0 && wfin) ? bracket_mono<MAXV, true>(c, w, ff.zt, L, d, hint0, zfdn, zfup)
-                                   : bracket_scan<MAXV, true>(c, w, ff.zt, L, d, zfdn, zfup);
-    const int lb = (c.mono1 && wfin) ? bracket_mono<MAXV, true>(c, w, fb.zt, L, d, hint1, zbdn, zbup)
-                                   : bracket_scan<MAXV, true>(c, w, fb.zt, L, d, zbdn, zbup);
+    Pair F, B;
+    const int lf = layer_eval<MAXV, true>(c, w, c.mono0 && wfin, ff, L, d, hint0, F);
+    const int lb = layer_eval<MAXV, true>(c, w, c.mono1 && wfin, fb, L, d, hint1, B);
     if (lf < 0 || lb < 0) return false;
-    const double xf = dmax(zfdn, dmin(d, zfup));
-    const double denf = zfup - zfdn;
+    const double xf = dmax(F.zk, dmin(d, F.zm));
+    const double denf = F.zm - F.zk;
     if (fabs(denf) < 1e-12) return false;
-    const double tf = (xf - zfdn) / denf;
-    const double xb = dmax(zbdn, dmin(d, zbup));
-    const double denb = zbup - zbdn;
+    const double tf = (xf - F.zk) / denf;
+    const double xb = dmax(B.zk, dmin(d, B.zm));
+    const double denb = B.zm - B.zk;
     if (fabs(denb) < 1e-12) return false;
-    const double tb = (xb - zbdn) / denb;
-    double ax, ay, az, bx, by, bz;
-    vel_at<MAXV>(c, w, ff.vel, L, lf, ax, ay, az);
-    vel_at<MAXV>(c, w, ff.vel, L, lf - 1, bx, by, bz);
-    const double fx = bx * tf + ax * (1.0 - tf), fy = by * tf + ay * (1.0 - tf), fz = bz * tf + az * (1.0 - tf);
-    vel_at<MAXV>(c, w, fb.vel, L, lb, ax, ay, az);
-    vel_at<MAXV>(c, w, fb.vel, L, lb - 1, bx, by, bz);
-    const double gx = bx * tb + ax * (1.0 - tb), gy = by * tb + ay * (1.0 - tb), gz = bz * tb + az * (1.0 - tb);
+    const double tb = (xb - B.zk) / denb;
+    const double fx = F.um0 * tf + F.uk0 * (1.0 - tf), fy = F.um1 * tf + F.uk1 * (1.0 - tf),
+                 fz = F.um2 * tf + F.uk2 * (1.0 - tf);
+    const double gx = B.um0 * tb + B.uk0 * (1.0 - tb), gy = B.um1 * tb + B.uk1 * (1.0 - tb),
+                 gz = B.um2 * tb + B.uk2 * (1.0 - tb);
     hx = gx * alpha + fx * (1.0 - alpha);
     hy = gy * alpha + fy * (1.0 - alpha);
     hz = gz * alpha + fz * (1.0 - alpha);
-    const int Lp1 = L + 1;
-    int dnf = lf, upf = (lf > 0) ? lf - 1 : 0, dnb = lb, upb = (lb > 0) ? lb - 1 : 0;
-    if (dnf >= Lp1) dnf = Lp1 - 1;
-    if (upf >= Lp1) upf = Lp1 - 1;
-    if (dnb >= Lp1) dnb = Lp1 - 1;
-    if (upb >= Lp1) upb = Lp1 - 1;
-    const double wdnf = attr_at<MAXV>(c, w, ff.w, Lp1, dnf), wupf = attr_at<MAXV>(c, w, ff.w, Lp1, upf);
-    const double wf = tf * wupf + (1.0 - tf) * wdnf;
-    const double wdnb = attr_at<MAXV>(c, w, fb.w, Lp1, dnb), wupb = attr_at<MAXV>(c, w, fb.w, Lp1, upb);
-    const double wb = tb * wupb + (1.0 - tb) * wdnb;
+    const double wf = tf * F.wm + (1.0 - tf) * F.wk;
+    const double wb = tb * B.wm + (1.0 - tb) * B.wk;
     wv = alpha * wb + (1.0 - alpha) * wf;
     return true;
 }
@@ -605,30 +650,34 @@ __global__ void MOPS_TRAJ_BOUNDS traj_kernel(TrajArgs a) {
     for (int64_t step = a.step_begin; step < a.step_end; ++step) {
         if (step == 0) {  // first_loop (:892-901)
             if (cell < 0 || cell >= C) { died = 0; break; }
-            dev::load_cell<MAXV>(c, cell, a.cellrec, a.vxyz, a.mono0, a.mono1);
+            dev::load_cell<MAXV>(c, cell, a.cellrec, a.vxyz, a.mono0, a.mono1, a.cxyz);
             double* r0 = a.rec;
             r0[0 * a.rec_stride + pid] = x;
             r0[1 * a.rec_stride + pid] = y;
             r0[2 * a.rec_stride + pid] = z;
         } else {  // one-hop nearest-centre walk (:902-922)
             if (cell < 0 || cell >= C) { died = (int)step; break; }
-            if (c.id != cell) dev::load_cell<MAXV>(c, cell, a.cellrec, a.vxyz, a.mono0, a.mono1);
-            double best = 1.7976931348623157e308;
-            int nc = cell;
-#pragma unroll
-            for (int n = 0; n <= MAXV; ++n) {
-                if (n <= c.nv) {
-                    int cid;
-                    if (n < MAXV) cid = (n < c.nv) ? c.coc[n] : cell; else cid = cell;
+            if (c.id != cell) dev::load_cell<MAXV>(c, cell, a.cellrec, a.vxyz, a.mono0, a.mono1, a.cxyz);
+            // Exact shortcut: if |p - c| < rs (half the distance to the nearest
+            // neighbour centre, minus 1 m), every neighbour is strictly farther
+            // than the current centre by far more than rounding, so the
+            // reference's argmin (current cell listed last, strict <) keeps c.
+            const double ex = x - c.cx, ey = y - c.cy, ez = z - c.cz;
+            if (!(ex * ex + ey * ey + ez * ez < c.rs2)) {
+                const int* rec = a.cellrec + (int64_t)cell * (((1 + 2 * MAXV) + 3) / 4 * 4);
+                double best = 1.7976931348623157e308;
+                int nc = cell;
+                for (int n = 0; n <= c.nv; ++n) {
+                    const int cid = (n < c.nv) ? rec[1 + MAXV + n] : cell;
                     if (cid >= 0 && cid < C) {
                         const double4 q = a.cxyz[cid];
                         const double l = dev::len3(q.x - x, q.y - y, q.z - z);
                         if (l < best) { best = l; nc = cid; }
                     }
                 }
+                cell = nc;
+                if (c.id != cell) dev::load_cell<MAXV>(c, cell, a.cellrec, a.vxyz, a.mono0, a.mono1, a.cxyz);
             }
-            cell = nc;
-            if (c.id != cell) dev::load_cell<MAXV>(c, cell, a.cellrec, a.vxyz, a.mono0, a.mono1);
         }
         const double d = -1.0 * (double)dep;
         const double r = dev::len3(x, y, z);
@@ -950,6 +999,24 @@ __global__ void mono_kernel(int64_t C, int maxv, int rec_ints, const int* cellre
     mono[i] = ok ? 1 : 0;
 }
 
+__global__ void pair_record_kernel(int64_t V, int L, const double* zt, const double* vel, const double* w,
+                                   double* pr) {
+    const int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (idx >= V * (L - 1)) return;
+    const int64_t v = idx / (L - 1);
+    const int k = (int)(idx % (L - 1)) + 1;
+    double2* o = reinterpret_cast<double2*>(pr + idx * 12);
+    const double* z = zt + v * L;
+    const double* ww = w + v * (L + 1);
+    const double* u = vel + (v * L + k - 1) * 3;
+    o[0] = make_double2(z[0], z[k - 1]);
+    o[1] = make_double2(z[k], ww[k - 1]);
+    o[2] = make_double2(ww[k], u[0]);
+    o[3] = make_double2(u[1], u[2]);
+    o[4] = make_double2(u[3], u[4]);
+    o[5] = make_double2(u[5], 0.0);
+}
+
 __device__ __forceinline__ uint64_t spread3(uint64_t v) {  // 21 bits -> every third bit
     v &= 0x1fffffULL;
     v = (v | (v << 32)) & 0x1f00000000ffffULL;
@@ -1037,6 +1104,7 @@ void free_mesh(mops_mesh* m) {
 void free_field(mops_field* f) {
     if (!f) return;
     (void)hipFree(f->d_zt); (void)hipFree(f->d_vel); (void)hipFree(f->d_w); (void)hipFree(f->d_mono);
+    (void)hipFree(f->d_pr);
     delete f;
 }
 
@@ -1105,7 +1173,34 @@ mops_status mops_mesh_create(const mops_mesh_desc* desc, void* stream, mops_mesh
     int64_t acc = 0;
     mops_status st;
     if ((st = upload(rec.data(), rec.size(), &m->d_cellrec, &acc, s)) != MOPS_OK) { free_mesh(m); return st; }
-    if ((st = upload_xyz(desc->h_cell_coord, C, &m->d_cxyz, &acc, s)) != MOPS_OK) { free_mesh(m); return st; }
+    {
+        // cell centres + squared "stay" radius rs^2 in .w: rs = half the
+        // distance to the nearest valid neighbour centre, shrunk by 1e-9
+        // relative and 1 m absolute (>> rounding of |p - c| at Earth radius)
+        std::vector<double4> cc((size_t)C);
+        const double* h = desc->h_cell_coord;
+        for (int64_t c = 0; c < C; ++c) {
+            double dmin = INFINITY;
+            const int ne = rec[c * m->rec_ints];
+            for (int k = 0; k < ne; ++k) {
+                const int nb = rec[c * m->rec_ints + 1 + m->maxv + k];
+                if (nb < 0) continue;
+                const double dx = h[3 * nb] - h[3 * c], dy = h[3 * nb + 1] - h[3 * c + 1], dz = h[3 * nb + 2] - h[3 * c + 2];
+                dmin = std::min(dmin, std::sqrt(dx * dx + dy * dy + dz * dz));
+            }
+            double rs2;
+            if (dmin == INFINITY) rs2 = INFINITY;  // no neighbour: the walk can only keep c
+            else {
+                const double rs = 0.5 * dmin * (1.0 - 1e-9) - 1.0;
+                rs2 = (rs > 0.0) ? rs * rs : 0.0;
+            }
+            cc[c] = make_double4(h[3 * c], h[3 * c + 1], h[3 * c + 2], rs2);
+        }
+        if ((st = dmalloc(&m->d_cxyz, (size_t)C, &acc)) != MOPS_OK) { free_mesh(m); return st; }
+        hipError_t e2 = hipMemcpyAsync(m->d_cxyz, cc.data(), C * sizeof(double4), hipMemcpyHostToDevice, s);
+        if (e2 == hipSuccess) e2 = hipStreamSynchronize(s);
+        if (e2 != hipSuccess) { free_mesh(m); return fail(MOPS_ERR_HIP, hipGetErrorString(e2)); }
+    }
     if ((st = upload_xyz(desc->h_vertex_coord, V, &m->d_vxyz, &acc, s)) != MOPS_OK) { free_mesh(m); return st; }
     if (desc->h_cells_on_vertex) {
         std::vector<int> cov((size_t)V * 3);
@@ -1171,6 +1266,10 @@ void mops_mesh_destroy(mops_mesh* mesh) { free_mesh(mesh); }
 int64_t mops_mesh_bytes(const mops_mesh* mesh) { return mesh ? mesh->bytes : 0; }
 
 static mops_status compute_mono(const mops_mesh* mesh, mops_field* f, hipStream_t s) {
+    const int64_t npr = mesh->V * (int64_t)std::max(mesh->L - 1, 0);
+    MOPS_TRY(dmalloc(&f->d_pr, (size_t)std::max<int64_t>(npr * 12, 1), &f->bytes));
+    if (npr > 0)
+        pair_record_kernel<<<grid_for(npr), kBlock, 0, s>>>(mesh->V, mesh->L, f->d_zt, f->d_vel, f->d_w, f->d_pr);
     MOPS_TRY(dmalloc(&f->d_mono, (size_t)mesh->C, &f->bytes));
     mono_kernel<<<grid_for(mesh->C), kBlock, 0, s>>>(mesh->C, mesh->maxv, mesh->rec_ints, mesh->d_cellrec, f->d_zt,
                                                     mesh->L, f->d_mono);
@@ -1357,8 +1456,8 @@ mops_status mops_traj_advance(const mops_mesh* mesh, const mops_field* front, co
     TrajArgs a;
     a.cellrec = mesh->d_cellrec; a.cxyz = mesh->d_cxyz; a.vxyz = mesh->d_vxyz;
     a.C = (int)mesh->C; a.V = (int)mesh->V; a.L = mesh->L;
-    a.f0 = dev::Field{front->d_zt, front->d_vel, front->d_w};
-    a.f1 = back ? dev::Field{back->d_zt, back->d_vel, back->d_w} : a.f0;
+    a.f0 = dev::Field{front->d_zt, front->d_pr};
+    a.f1 = back ? dev::Field{back->d_zt, back->d_pr} : a.f0;
     a.mono0 = front->d_mono;
     a.mono1 = back ? back->d_mono : front->d_mono;
     a.order = p->d_order;
