@@ -42,6 +42,8 @@ def parse():
     p.add_argument("--duration", type=int, default=86400)
     p.add_argument("--record", type=int, default=3600)
     p.add_argument("--method", choices=["euler", "rk4"], default="euler")
+    p.add_argument("--mode", choices=["streamline", "pathline"], default="streamline",
+                   help="pathline: two snapshots (front/back), BASELINE config 3 shape")
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--cpu-seconds", type=float, default=12.0, help="target CPU-baseline sample length")
     return p.parse_args()
@@ -72,6 +74,8 @@ def main():
     snap = synth.make_snapshot(mesh, timestep=0)
     dmesh = DeviceMesh.from_mesh(mesh)
     dfield = DeviceField.from_snapshot(dmesh, snap)
+    pathline = args.mode == "pathline"
+    dback = DeviceField.from_snapshot(dmesh, synth.make_snapshot(mesh, timestep=1, phase=0.35)) if pathline else None
     # seeds: uniform on |lat| < 70 deg, rejected on land, one shard per rank
     rng_seed = 12345 + rank
     seeds = synth.uniform_band_seeds(int(args.particles * 1.25) + 64, seed=rng_seed)
@@ -82,7 +86,7 @@ def main():
     cfg = TrajectoryConfig(deltaT=args.dt, simulationDuration=args.duration, recordT=args.record, depth=args.depth,
                            method=1 if args.method == "euler" else 0)
     ps = ParticleSet(dmesh, seeds, args.depth, cfg, device=dev)
-    period = ps.record_period(pathline=False)
+    period = ps.record_period(pathline=pathline)
     n_steps = cfg.n_steps
     bounds = list(range(0, n_steps, period)) + [n_steps]
     segments = [(bounds[i], bounds[i + 1]) for i in range(len(bounds) - 1)]
@@ -105,7 +109,7 @@ def main():
                 if timed:
                     e0 = torch.cuda.Event(enable_timing=True); e1 = torch.cuda.Event(enable_timing=True)
                     e0.record(compute)
-                ps.advance(dfield, None, s0, s1, stream=compute)
+                ps.advance(dfield, dback, s0, s1, stream=compute)
                 if timed:
                     e1.record(compute)
                     kernel_ms.append((e0, e1))
@@ -151,7 +155,7 @@ def main():
 
     value = attempted_all * args.steps / elapsed
     nv_mean = float(np.mean(mesh.nEdgesOnCell.astype(np.float64)))
-    B = algorithmic_bytes_per_pstep(nv_mean, mesh.nVertLevels, 1)
+    B = algorithmic_bytes_per_pstep(nv_mean, mesh.nVertLevels, 2 if pathline else 1)
     psteps_per_launch = attempted / len(segments)
     achieved = B * psteps_per_launch / avg_kernel_s / 1e9
     traffic = None
@@ -159,14 +163,15 @@ def main():
     if os.path.exists(pmc_path):
         try:
             pm = json.load(open(pmc_path))
-            if pm.get("workload") == f"ec30to60_streamline_{args.method}_{args.particles}":
+            if pm.get("workload") == f"ec30to60_{args.mode}_{args.method}_{args.particles}":
                 traffic = pm.get("bytes_per_launch")
         except Exception:
             traffic = None
 
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        cpu = cpu_baseline(mesh, snap, seeds, ps.cell.cpu().numpy(), args, n_steps)
+        back_snap = synth.make_snapshot(mesh, timestep=1, phase=0.35) if pathline else None
+        cpu = cpu_baseline(mesh, snap, back_snap, seeds, ps.cell.cpu().numpy(), args, n_steps)
 
     if rank == 0:
         line = {
@@ -183,7 +188,8 @@ def main():
             "dtype": "f64",
             "data": "synthetic (icosahedral-dual Voronoi mesh, analytic flow; no MPAS files offline)",
             "config": {
-                "workload": "EC30to60-class streamline, 1e6 particles/GPU, depth 800 m, dt 120 s, 1 day",
+                "workload": (f"EC30to60-class {args.mode}, {n:.0e} particles/GPU, depth {args.depth:g} m, "
+                             f"dt {args.dt} s, {args.duration / 86400:g} day"),
                 "cells": mesh.nCells, "vertices": mesh.nVertices, "levels": mesh.nVertLevels,
                 "particles_per_gpu": n, "particles_total": int(n_all), "integration_steps": n_steps,
                 "records": ps.K, "method": args.method, "parallelism": f"particle-shard x{world}",
@@ -199,8 +205,8 @@ def main():
                 "unit": "GB/s",
                 "frac": achieved / PEAK_HBM_GBS,
                 "traffic": traffic,
-                "kernel": "traj_kernel<7,false,true> (streamline Euler)" if args.method == "euler"
-                else "traj_kernel<7,false,false> (streamline RK4)",
+                "kernel": f"traj_kernel<7,{str(pathline).lower()},{str(args.method == 'euler').lower()}> "
+                          f"({args.mode} {args.method})",
                 "algorithmic_bytes_per_particle_step": B,
                 "particle_steps_per_launch": psteps_per_launch,
                 "avg_launch_ms": avg_kernel_s * 1e3,
@@ -212,7 +218,7 @@ def main():
         dist.destroy_process_group()
 
 
-def cpu_baseline(mesh, snap, seeds, cells, args, n_steps):
+def cpu_baseline(mesh, snap, back_snap, seeds, cells, args, n_steps):
     """The CPU oracle (port of the TBB path) on this host's cores, bounded sample."""
     try:
         from oracle import oracle as O
@@ -221,22 +227,23 @@ def cpu_baseline(mesh, snap, seeds, cells, args, n_steps):
     threads = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or (os.cpu_count() or 1)
     threads = max(1, min(threads, os.cpu_count() or 1))
     derived = O.preprocess(mesh, snap)
+    back = O.preprocess(mesh, back_snap) if back_snap is not None else None
     euler = args.method == "euler"
     # calibrate on a small sample, then size the timed sample to ~cpu_seconds
     n0 = min(4000, len(seeds))
     t = time.perf_counter()
-    O.run(mesh, derived, None, seeds[:n0], depth=args.depth, delta_t=args.dt, duration=args.duration,
+    O.run(mesh, derived, back, seeds[:n0], depth=args.depth, delta_t=args.dt, duration=args.duration,
           record_t=args.record, euler=euler, cells=cells[:n0], n_threads=threads, finalize=False)
     rate = n0 * n_steps / max(time.perf_counter() - t, 1e-6)
     n1 = int(min(len(seeds), max(n0, rate * args.cpu_seconds / n_steps)))
     t = time.perf_counter()
-    out = O.run(mesh, derived, None, seeds[:n1], depth=args.depth, delta_t=args.dt, duration=args.duration,
+    out = O.run(mesh, derived, back, seeds[:n1], depth=args.depth, delta_t=args.dt, duration=args.duration,
                 record_t=args.record, euler=euler, cells=cells[:n1], n_threads=threads, finalize=False)
     dt = time.perf_counter() - t
     death = out["death"].astype(np.int64)
     attempted = np.where(death < 0, n_steps, death + 1).sum()
     return {"value": float(attempted / dt), "unit": "particle-steps/s", "cores": threads, "kind": "port",
-            "sample": f"{n1} of the same seeds x {n_steps} steps ({args.method}), same mesh/field, "
+            "sample": f"{n1} of the same seeds x {n_steps} steps ({args.mode} {args.method}), same mesh/fields, "
                       f"OpenMP schedule(dynamic,16) over particles; {dt:.1f} s"}
 
 

@@ -58,6 +58,10 @@ mops_status fail(mops_status st, const std::string& msg) {
 constexpr int kMaxLevels = 100;  // reference MAX_VERTICAL_LEVEL_NUM
 constexpr int kMaxVertex = 20;   // reference MAX_VERTEX_NUM
 constexpr int kBlock = 256;
+#ifndef MOPS_TRAJ_BLOCK
+#define MOPS_TRAJ_BLOCK 64  // one wave per workgroup: a slow wave never holds a block's slots
+#endif
+constexpr int kTrajBlock = MOPS_TRAJ_BLOCK;
 
 inline int rec_ints_for(int maxv) { return ((1 + 2 * maxv) + 3) / 4 * 4; }
 
@@ -619,17 +623,27 @@ struct TrajArgs {
     int64_t rec_stride;
 };
 
-#ifndef MOPS_TRAJ_WAVES_PER_EU
-#define MOPS_TRAJ_WAVES_PER_EU 0
+// Minimum waves per SIMD requested per instantiation (register budget vs
+// latency hiding; swept on MI355X with tools/occupancy_sweep.sh).
+#ifndef MOPS_W_SE
+#define MOPS_W_SE 3  // streamline Euler
 #endif
-#if MOPS_TRAJ_WAVES_PER_EU > 0
-#define MOPS_TRAJ_BOUNDS __launch_bounds__(kBlock, MOPS_TRAJ_WAVES_PER_EU)
-#else
-#define MOPS_TRAJ_BOUNDS __launch_bounds__(kBlock)
+#ifndef MOPS_W_SR
+#define MOPS_W_SR 1  // streamline RK4
 #endif
+#ifndef MOPS_W_PE
+#define MOPS_W_PE 1  // pathline Euler
+#endif
+#ifndef MOPS_W_PR
+#define MOPS_W_PR 2  // pathline RK4
+#endif
+template <bool PATH, bool EULER>
+struct TrajWaves {
+    static constexpr int value = PATH ? (EULER ? MOPS_W_PE : MOPS_W_PR) : (EULER ? MOPS_W_SE : MOPS_W_SR);
+};
 
 template <int MAXV, bool PATH, bool EULER>
-__global__ void MOPS_TRAJ_BOUNDS traj_kernel(TrajArgs a) {
+__global__ void __launch_bounds__(kTrajBlock, (TrajWaves<PATH, EULER>::value)) traj_kernel(TrajArgs a) {
     // XCD-aware mapping: blocks b, b+8, ... share an XCD (L2); give each XCD a
     // contiguous range of the locality-ordered particles (bijective remap)
     const unsigned nblk = gridDim.x, b = blockIdx.x, xcd = b % 8u, q = nblk / 8u, r = nblk % 8u;
@@ -1117,13 +1131,13 @@ int64_t gcd64(int64_t a, int64_t b) {
 
 template <int MAXV>
 void launch_traj(const TrajArgs& a, bool path, bool euler, hipStream_t s) {
-    const unsigned g = grid_for(a.n);
+    const unsigned g = (unsigned)((a.n + kTrajBlock - 1) / kTrajBlock);
     if (path) {
-        if (euler) traj_kernel<MAXV, true, true><<<g, kBlock, 0, s>>>(a);
-        else traj_kernel<MAXV, true, false><<<g, kBlock, 0, s>>>(a);
+        if (euler) traj_kernel<MAXV, true, true><<<g, kTrajBlock, 0, s>>>(a);
+        else traj_kernel<MAXV, true, false><<<g, kTrajBlock, 0, s>>>(a);
     } else {
-        if (euler) traj_kernel<MAXV, false, true><<<g, kBlock, 0, s>>>(a);
-        else traj_kernel<MAXV, false, false><<<g, kBlock, 0, s>>>(a);
+        if (euler) traj_kernel<MAXV, false, true><<<g, kTrajBlock, 0, s>>>(a);
+        else traj_kernel<MAXV, false, false><<<g, kTrajBlock, 0, s>>>(a);
     }
 }
 
