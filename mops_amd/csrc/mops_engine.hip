@@ -81,6 +81,7 @@ struct mops_mesh {
     uint64_t* d_bkeys = nullptr;  // sorted bucket keys [C]
     int* d_bcells = nullptr;      // cell ids in key order [C]
     uint64_t* d_cell_key = nullptr;  // Morton key of each cell centre (particle locality order)
+    double* d_cellB = nullptr;       // [C][maxv] Wachspress B_i of each cell polygon
     // grow-only scratch for mops_order_particles (not re-entrant, like the reference's global app)
     mutable void* d_scratch = nullptr;
     mutable size_t scratch_bytes = 0;
@@ -147,6 +148,10 @@ __device__ __forceinline__ double dmax(double a, double b) { return (a < b) ? b 
 __device__ __forceinline__ double dmin(double a, double b) { return (b < a) ? b : a; }  // std::min
 __device__ __forceinline__ double dclamp(double v, double lo, double hi) { return (v < lo) ? lo : (hi < v) ? hi : v; }
 
+#ifndef MOPS_CELL_REGCACHE
+#define MOPS_CELL_REGCACHE 1  // 1: polygon xyz + B_i live in registers across steps; 0: re-read per evaluation
+#endif
+
 // Per-cell stencil cached in registers while the particle stays in the cell.
 template <int MAXV>
 struct Cell {
@@ -156,14 +161,20 @@ struct Cell {
     double cx, cy, cz;  // cell centre
     double rs2;         // squared "stay" radius (see traj_kernel's walk)
     int vid[MAXV];
+#if MOPS_CELL_REGCACHE
     double x[MAXV], y[MAXV], z[MAXV];
     double B[MAXV];  // Wachspress B_i = area(poly[i-1], poly[i], poly[i+1]) (depends on the polygon only)
+#else
+    const double4* __restrict__ vxyz;   // polygon re-read per evaluation (L1-resident)
+    const double* __restrict__ cellB;   // per-cell B_i [C][MAXV], computed by cell_b_kernel
+#endif
 };
 
 template <int MAXV>
 __device__ __forceinline__ void load_cell(Cell<MAXV>& c, int cell, const int* __restrict__ cellrec,
                                           const double4* __restrict__ vxyz, const uint8_t* __restrict__ mono0,
-                                          const uint8_t* __restrict__ mono1, const double4* __restrict__ cxyz) {
+                                          const uint8_t* __restrict__ mono1, const double4* __restrict__ cxyz,
+                                          const double* __restrict__ cellB) {
     c.mono0 = mono0[cell] != 0;
     c.mono1 = mono1[cell] != 0;
     {
@@ -181,6 +192,7 @@ __device__ __forceinline__ void load_cell(Cell<MAXV>& c, int cell, const int* __
     c.id = cell;
     c.nv = buf[0];
     const int nv = c.nv;
+#if MOPS_CELL_REGCACHE
 #pragma unroll
     for (int k = 0; k < MAXV; ++k) {
         c.vid[k] = buf[1 + k];
@@ -210,6 +222,13 @@ __device__ __forceinline__ void load_cell(Cell<MAXV>& c, int cell, const int* __
             c.B[i] = 0.0;
         }
     }
+    (void)cellB;
+#else
+#pragma unroll
+    for (int k = 0; k < MAXV; ++k) c.vid[k] = buf[1 + k];
+    c.vxyz = vxyz;
+    c.cellB = cellB;
+#endif
 }
 
 // guards + TBBKernel::IsInMesh + Interpolator::CalcPolygonWachspress
@@ -221,16 +240,31 @@ __device__ __forceinline__ bool weights(const Cell<MAXV>& c, int L, int V, doubl
     const int nv = c.nv;
     if (nv <= 0 || nv > kMaxVertex) return false;
     if (!isfinite(px) || !isfinite(py) || !isfinite(pz)) return false;
+#if MOPS_CELL_REGCACHE
+    const double* X = c.x; const double* Y = c.y; const double* Z = c.z; const double* BB = c.B;
+#else
+    double X[MAXV], Y[MAXV], Z[MAXV], BB[MAXV];
+#pragma unroll
+    for (int k = 0; k < MAXV; ++k) {
+        if (k < nv) {
+            const double4 q = c.vxyz[c.vid[k]];
+            X[k] = q.x; Y[k] = q.y; Z[k] = q.z;
+            BB[k] = c.cellB[(int64_t)c.id * MAXV + k];
+        } else {
+            X[k] = 0.0; Y[k] = 0.0; Z[k] = 0.0; BB[k] = 0.0;
+        }
+    }
+#endif
 #pragma unroll
     for (int k = 0; k < MAXV; ++k) {
         if (k < nv) {
             const bool wrap = (k + 1 >= nv);
-            const double bx = wrap ? c.x[0] : c.x[(k + 1) % MAXV];
-            const double by = wrap ? c.y[0] : c.y[(k + 1) % MAXV];
-            const double bz = wrap ? c.z[0] : c.z[(k + 1) % MAXV];
-            const double nx = c.y[k] * bz - c.z[k] * by;
-            const double ny = c.z[k] * bx - c.x[k] * bz;
-            const double nz = c.x[k] * by - c.y[k] * bx;
+            const double bx = wrap ? X[0] : X[(k + 1) % MAXV];
+            const double by = wrap ? Y[0] : Y[(k + 1) % MAXV];
+            const double bz = wrap ? Z[0] : Z[(k + 1) % MAXV];
+            const double nx = Y[k] * bz - Z[k] * by;
+            const double ny = Z[k] * bx - X[k] * bz;
+            const double nz = X[k] * by - Y[k] * bx;
             if (nx * px + ny * py + nz * pz < 0.0) return false;
         }
     }
@@ -242,19 +276,19 @@ __device__ __forceinline__ bool weights(const Cell<MAXV>& c, int L, int V, doubl
     double lx = 0, ly = 0, lz = 0;
 #pragma unroll
     for (int k = 0; k < MAXV; ++k)
-        if (k == nv - 1) { lx = c.x[k]; ly = c.y[k]; lz = c.z[k]; }
+        if (k == nv - 1) { lx = X[k]; ly = Y[k]; lz = Z[k]; }
     double sum = 0.0;
-    double Anext = tri_area(lx, ly, lz, c.x[0], c.y[0], c.z[0], px, py, pz);
+    double Anext = tri_area(lx, ly, lz, X[0], Y[0], Z[0], px, py, pz);
 #pragma unroll
     for (int i = 0; i < MAXV; ++i) {
         if (i < nv) {
             const double Ai = Anext;
             const bool wrap = (i + 1 >= nv);
-            const double nx = wrap ? c.x[0] : c.x[(i + 1) % MAXV];
-            const double ny = wrap ? c.y[0] : c.y[(i + 1) % MAXV];
-            const double nz = wrap ? c.z[0] : c.z[(i + 1) % MAXV];
-            Anext = tri_area(c.x[i], c.y[i], c.z[i], nx, ny, nz, px, py, pz);
-            w[i] = c.B[i] / (Ai * Anext);
+            const double nx = wrap ? X[0] : X[(i + 1) % MAXV];
+            const double ny = wrap ? Y[0] : Y[(i + 1) % MAXV];
+            const double nz = wrap ? Z[0] : Z[(i + 1) % MAXV];
+            Anext = tri_area(X[i], Y[i], Z[i], nx, ny, nz, px, py, pz);
+            w[i] = BB[i] / (Ai * Anext);
             sum += w[i];
         } else {
             w[i] = 0.0;
@@ -609,6 +643,7 @@ struct TrajArgs {
     const uint8_t* __restrict__ mono0;
     const uint8_t* __restrict__ mono1;
     const int* __restrict__ order;  // slot -> particle (NULL = identity)
+    const double* __restrict__ cellB;  // per-cell Wachspress B_i
     double* px; double* py; double* pz;
     float* depth;
     int* cell;
@@ -664,14 +699,14 @@ __global__ void __launch_bounds__(kTrajBlock, (TrajWaves<PATH, EULER>::value)) t
     for (int64_t step = a.step_begin; step < a.step_end; ++step) {
         if (step == 0) {  // first_loop (:892-901)
             if (cell < 0 || cell >= C) { died = 0; break; }
-            dev::load_cell<MAXV>(c, cell, a.cellrec, a.vxyz, a.mono0, a.mono1, a.cxyz);
+            dev::load_cell<MAXV>(c, cell, a.cellrec, a.vxyz, a.mono0, a.mono1, a.cxyz, a.cellB);
             double* r0 = a.rec;
             r0[0 * a.rec_stride + pid] = x;
             r0[1 * a.rec_stride + pid] = y;
             r0[2 * a.rec_stride + pid] = z;
         } else {  // one-hop nearest-centre walk (:902-922)
             if (cell < 0 || cell >= C) { died = (int)step; break; }
-            if (c.id != cell) dev::load_cell<MAXV>(c, cell, a.cellrec, a.vxyz, a.mono0, a.mono1, a.cxyz);
+            if (c.id != cell) dev::load_cell<MAXV>(c, cell, a.cellrec, a.vxyz, a.mono0, a.mono1, a.cxyz, a.cellB);
             // Exact shortcut: if |p - c| < rs (half the distance to the nearest
             // neighbour centre, minus 1 m), every neighbour is strictly farther
             // than the current centre by far more than rounding, so the
@@ -690,7 +725,7 @@ __global__ void __launch_bounds__(kTrajBlock, (TrajWaves<PATH, EULER>::value)) t
                     }
                 }
                 cell = nc;
-                if (c.id != cell) dev::load_cell<MAXV>(c, cell, a.cellrec, a.vxyz, a.mono0, a.mono1, a.cxyz);
+                if (c.id != cell) dev::load_cell<MAXV>(c, cell, a.cellrec, a.vxyz, a.mono0, a.mono1, a.cxyz, a.cellB);
             }
         }
         const double d = -1.0 * (double)dep;
@@ -1013,6 +1048,42 @@ __global__ void mono_kernel(int64_t C, int maxv, int rec_ints, const int* cellre
     mono[i] = ok ? 1 : 0;
 }
 
+// Wachspress B_i = area(poly[i-1], poly[i], poly[i+1]) per cell, with the
+// same device arithmetic as the in-kernel computation (bit-identical).
+template <int MAXV>
+__global__ void cell_b_kernel(int64_t C, const int* cellrec, const double4* vxyz, double* cellB) {
+    const int64_t c = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (c >= C) return;
+    constexpr int REC = ((1 + 2 * MAXV) + 3) / 4 * 4;
+    const int* r = cellrec + c * REC;
+    const int nv = r[0];
+    double x[MAXV], y[MAXV], z[MAXV];
+#pragma unroll
+    for (int k = 0; k < MAXV; ++k) {
+        if (k < nv) { const double4 p = vxyz[r[1 + k]]; x[k] = p.x; y[k] = p.y; z[k] = p.z; }
+        else { x[k] = 0.0; y[k] = 0.0; z[k] = 0.0; }
+    }
+    double lx = 0, ly = 0, lz = 0;
+#pragma unroll
+    for (int k = 0; k < MAXV; ++k)
+        if (k == nv - 1) { lx = x[k]; ly = y[k]; lz = z[k]; }
+#pragma unroll
+    for (int i = 0; i < MAXV; ++i) {
+        double b = 0.0;
+        if (i < nv) {
+            const double qx = (i == 0) ? lx : x[(i + MAXV - 1) % MAXV];
+            const double qy = (i == 0) ? ly : y[(i + MAXV - 1) % MAXV];
+            const double qz = (i == 0) ? lz : z[(i + MAXV - 1) % MAXV];
+            const bool wrap = (i + 1 >= nv);
+            const double nx = wrap ? x[0] : x[(i + 1) % MAXV];
+            const double ny = wrap ? y[0] : y[(i + 1) % MAXV];
+            const double nz = wrap ? z[0] : z[(i + 1) % MAXV];
+            b = dev::tri_area(qx, qy, qz, x[i], y[i], z[i], nx, ny, nz);
+        }
+        cellB[c * MAXV + i] = b;
+    }
+}
+
 __global__ void pair_record_kernel(int64_t V, int L, const double* zt, const double* vel, const double* w,
                                    double* pr) {
     const int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -1110,7 +1181,7 @@ mops_status upload(const T* h, size_t count, T** d, int64_t* acc, hipStream_t s)
 void free_mesh(mops_mesh* m) {
     if (!m) return;
     (void)hipFree(m->d_cellrec); (void)hipFree(m->d_cxyz); (void)hipFree(m->d_vxyz); (void)hipFree(m->d_cov);
-    (void)hipFree(m->d_bkeys); (void)hipFree(m->d_bcells); (void)hipFree(m->d_cell_key);
+    (void)hipFree(m->d_bkeys); (void)hipFree(m->d_bcells); (void)hipFree(m->d_cell_key); (void)hipFree(m->d_cellB);
     (void)hipFree(m->d_scratch);
     delete m;
 }
@@ -1268,6 +1339,12 @@ mops_status mops_mesh_create(const mops_mesh_desc* desc, void* stream, mops_mesh
     if (e != hipSuccess) { free_mesh(m); return fail(MOPS_ERR_HIP, std::string("bucket sort: ") + hipGetErrorString(e)); }
     if ((st = dmalloc(&m->d_cell_key, (size_t)C, &acc)) != MOPS_OK) { free_mesh(m); return st; }
     cell_key_kernel<<<grid_for(C), kBlock, 0, s>>>(C, m->d_cxyz, m->d_cell_key);
+    if ((st = dmalloc(&m->d_cellB, (size_t)(C * m->maxv), &acc)) != MOPS_OK) { free_mesh(m); return st; }
+    switch (m->maxv) {
+        case 7: cell_b_kernel<7><<<grid_for(C), kBlock, 0, s>>>(C, m->d_cellrec, m->d_vxyz, m->d_cellB); break;
+        case 12: cell_b_kernel<12><<<grid_for(C), kBlock, 0, s>>>(C, m->d_cellrec, m->d_vxyz, m->d_cellB); break;
+        default: cell_b_kernel<20><<<grid_for(C), kBlock, 0, s>>>(C, m->d_cellrec, m->d_vxyz, m->d_cellB); break;
+    }
     e = hipGetLastError();
     if (e == hipSuccess) e = hipStreamSynchronize(s);
     if (e != hipSuccess) { free_mesh(m); return fail(MOPS_ERR_HIP, std::string("cell keys: ") + hipGetErrorString(e)); }
@@ -1475,6 +1552,7 @@ mops_status mops_traj_advance(const mops_mesh* mesh, const mops_field* front, co
     a.mono0 = front->d_mono;
     a.mono1 = back ? back->d_mono : front->d_mono;
     a.order = p->d_order;
+    a.cellB = mesh->d_cellB;
     a.px = p->d_x; a.py = p->d_y; a.pz = p->d_z; a.depth = p->d_depth; a.cell = p->d_cell; a.death = p->d_death_step;
     a.n = p->n;
     a.step_begin = step_begin; a.step_end = step_end; a.n_steps = n_steps;
