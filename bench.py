@@ -159,12 +159,14 @@ def main():
     psteps_per_launch = attempted / len(segments)
     achieved = B * psteps_per_launch / avg_kernel_s / 1e9
     traffic = None
+    measured = None
     pmc_path = os.path.join(ROOT, "profiles", "pmc_traffic.json")
     if os.path.exists(pmc_path):
         try:
             pm = json.load(open(pmc_path))
             if pm.get("workload") == f"ec30to60_{args.mode}_{args.method}_{args.particles}":
                 traffic = pm.get("bytes_per_launch")
+                measured = traffic / avg_kernel_s / 1e9
         except Exception:
             traffic = None
 
@@ -208,6 +210,10 @@ def main():
                 "kernel": f"traj_kernel<7,{str(pathline).lower()},{str(args.method == 'euler').lower()}> "
                           f"({args.mode} {args.method})",
                 "algorithmic_bytes_per_particle_step": B,
+                "algorithmic_bytes_note": ("SURVEY.md 8(d) model: full zTop column (8*nv*L) per step; the engine "
+                                           "reads ~2 levels per step, so frac > 1 is possible -- see measured_*"),
+                "measured_hbm_gbs": measured,
+                "measured_frac": (measured / PEAK_HBM_GBS) if measured else None,
                 "particle_steps_per_launch": psteps_per_launch,
                 "avg_launch_ms": avg_kernel_s * 1e3,
             },

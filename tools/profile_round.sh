@@ -1,0 +1,15 @@
+#!/bin/bash
+# Full measurement for the round: bench (with CPU baseline), rocprofv3 kernel
+# stats of the same command, and FETCH/WRITE PMC passes for the roofline traffic.
+set -u
+out=${1:-gpurun_out/round}
+mkdir -p "$out"
+export TMPDIR=/tmp
+timeout -k 10 600 python3 bench.py ${BENCH_ARGS:-} > "$out/bench.json" 2> "$out/bench.err" || { echo "bench failed"; exit 1; }
+timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$out/stats" -o p -- \
+    python3 bench.py --no-cpu-baseline ${BENCH_ARGS:-} > "$out/stats.log" 2>&1 || { echo "stats failed"; exit 1; }
+timeout -k 5 150 rocprofv3 --pmc FETCH_SIZE --kernel-include-regex traj_kernel --output-format csv -d "$out/fetch" -o p -- \
+    python3 bench.py --no-cpu-baseline --steps 1 --warmup 0 ${BENCH_ARGS:-} > "$out/fetch.log" 2>&1 || { echo "fetch failed"; exit 1; }
+timeout -k 5 150 rocprofv3 --pmc WRITE_SIZE --kernel-include-regex traj_kernel --output-format csv -d "$out/write" -o p -- \
+    python3 bench.py --no-cpu-baseline --steps 1 --warmup 0 ${BENCH_ARGS:-} > "$out/write.log" 2>&1 || { echo "write failed"; exit 1; }
+echo "profile ok"
