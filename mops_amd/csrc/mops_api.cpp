@@ -1,0 +1,410 @@
+// mops_api.cpp -- the MOPS:: C++ operator API (include/mops/MOPS.h) on top
+// of the C ABI.  Mirrors the reference's MOPS.cpp / MOPSApp.cpp state machine
+// (src/Core/MOPS.cpp:10-71, src/Core/MOPSApp.cpp:34-337): one global app,
+// Init -> Begin -> AddGridMesh -> AddAttribute* -> End -> ActiveAttribute ->
+// RunStreamLine / RunPathLine.  Every trajectory computation goes to the HIP
+// engine; this file only marshals host containers.
+#include "mops/MOPS.h"
+
+#include <hip/hip_runtime.h>
+
+#include <chrono>
+#include <cmath>
+#include <cstdarg>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <iostream>
+#include <stdexcept>
+
+namespace MOPS {
+namespace {
+
+void Error(const char* fmt, ...) {
+    va_list ap;
+    va_start(ap, fmt);
+    std::fprintf(stderr, "[Error]: ");
+    std::vfprintf(stderr, fmt, ap);
+    std::fprintf(stderr, "\n");
+    va_end(ap);
+}
+
+// ---- TimerManager (src/Utils/Timer.hpp:17-216, categories only) ----------
+struct Timing {
+    std::map<std::string, double> by_category;
+    std::vector<std::pair<std::string, double>> records;
+    void add(const std::string& name, const std::string& cat, double ms) {
+        by_category[cat] += ms;
+        records.emplace_back(name, ms);
+    }
+};
+Timing g_timing;
+
+struct ScopedTimer {
+    std::string name, cat;
+    std::chrono::steady_clock::time_point t0 = std::chrono::steady_clock::now();
+    ScopedTimer(std::string n, std::string c) : name(std::move(n)), cat(std::move(c)) {}
+    ~ScopedTimer() {
+        const double ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+        g_timing.add(name, cat, ms);
+    }
+};
+
+enum class State { Idle, Configuring, Ready };
+
+struct App {
+    State state = State::Idle;
+    std::shared_ptr<MPASOGrid> grid;
+    std::map<int, std::shared_ptr<MPASOSolution>> sols;
+    mops_mesh* mesh = nullptr;
+    std::map<int, mops_field*> fields;
+    mops_field* front = nullptr;
+    mops_field* back = nullptr;
+
+    void release() {
+        for (auto& kv : fields) mops_field_destroy(kv.second);
+        fields.clear();
+        if (mesh) mops_mesh_destroy(mesh);
+        mesh = nullptr;
+        front = back = nullptr;
+    }
+    ~App() { release(); }
+};
+App g_app;
+
+void check(mops_status st, const char* what) {
+    if (st != MOPS_OK) throw std::runtime_error(std::string(what) + ": " + mops_last_error());
+}
+
+mops_field* make_field(const MPASOSolution& s) {
+    mops_snapshot_desc d{};
+    d.timestep = s.mTimesteps;
+    d.h_layer_thickness = s.cellLayerThickness_vec.empty() ? nullptr : s.cellLayerThickness_vec.data();
+    d.h_bottom_depth = s.cellBottomDepth_vec.empty() ? nullptr : s.cellBottomDepth_vec.data();
+    d.h_surface_height = s.cellSurfaceHeight_vec.empty() ? nullptr : s.cellSurfaceHeight_vec.data();
+    d.h_zonal_velocity = s.cellZonalVelocity_vec.empty() ? nullptr : s.cellZonalVelocity_vec.data();
+    d.h_meridional_velocity = s.cellMeridionalVelocity_vec.empty() ? nullptr : s.cellMeridionalVelocity_vec.data();
+    d.h_vert_velocity_top = s.cellVertVelocity_vec.empty() ? nullptr : s.cellVertVelocity_vec.data();
+    mops_field* f = nullptr;
+    check(mops_field_create(g_app.mesh, &d, nullptr, &f), "mops_field_create");
+    return f;
+}
+
+std::vector<TrajectoryLine> run(TrajectorySettings* config, std::vector<CartesianCoord>& pts, bool pathline,
+                                const char* stage) {
+    if (config == nullptr || g_app.front == nullptr || (pathline && g_app.back == nullptr)) {
+        Error("[%s] invalid inputs", stage);  // MPASOVisualizerKernels.cpp:659-662
+        return {};
+    }
+    if (pts.empty()) return {};
+    if (config->deltaT == 0 || config->recordT == 0 || config->simulationDuration == 0) {
+        Error("[%s] invalid trajectory settings", stage);  // :666-669
+        return {};
+    }
+    const int64_t n = (int64_t)pts.size();
+    const bool per_particle = config->hasPerParticleDepths() && config->particle_depths.size() == pts.size();
+    std::vector<float> depths(pts.size(), config->depth);  // BuildEffectiveDepths (TrajectoryCommon.h:29-41)
+    if (per_particle) depths = config->particle_depths;
+    mops_traj_cfg cfg{(int64_t)config->deltaT, (int64_t)config->simulationDuration, (int64_t)config->recordT,
+                      config->directionType == CalcDirection::kForward ? MOPS_FORWARD : MOPS_BACKWARD,
+                      config->methodType == CalcMethodType::kEuler ? MOPS_EULER : MOPS_RK4};
+    const int64_t K = mops_traj_num_records(&cfg), steps = mops_traj_num_steps(&cfg);
+    std::vector<TrajectoryLine> lines((size_t)n);
+    for (int64_t i = 0; i < n; ++i) {  // InitTrajectoryLines (:43-55)
+        auto& l = lines[(size_t)i];
+        l.lineID = (int)i;
+        l.points = {pts[(size_t)i]};
+        l.lastPoint = pts[(size_t)i];
+        l.duration = (double)config->simulationDuration;
+        l.timestamp = (double)config->deltaT;
+        l.depth = depths[(size_t)i];
+    }
+    if (K <= 0 || steps <= 0) {
+        Error("[%s] invalid integration steps", stage);  // :709-712 returns the seed-only lines
+        return lines;
+    }
+    const int64_t P = K + 1;
+    std::vector<double> hp((size_t)(n * P * 3)), hv((size_t)(n * P * 3)), ht((size_t)(n * P)), hs((size_t)(n * P)),
+        hl((size_t)(n * 3));
+    check(mops_run_trajectories(g_app.mesh, g_app.front, pathline ? g_app.back : nullptr, &cfg, n,
+                                reinterpret_cast<const double*>(pts.data()), depths.data(), config->depth, nullptr,
+                                hp.data(), hv.data(), ht.data(), hs.data(), hl.data(), nullptr, nullptr, nullptr,
+                                nullptr),
+          "mops_run_trajectories");
+    for (int64_t i = 0; i < n; ++i) {  // FinalizeTrajectoryLines[WithAttrs] + RemoveNaN (device-side)
+        auto& l = lines[(size_t)i];
+        l.points.resize((size_t)P);
+        l.velocity.resize((size_t)P);
+        l.temperature.resize((size_t)P);
+        l.salinity.resize((size_t)P);
+        for (int64_t j = 0; j < P; ++j) {
+            const size_t q = (size_t)((i * P + j) * 3);
+            l.points[(size_t)j] = {hp[q], hp[q + 1], hp[q + 2]};
+            l.velocity[(size_t)j] = {hv[q], hv[q + 1], hv[q + 2]};
+            l.temperature[(size_t)j] = ht[(size_t)(i * P + j)];
+            l.salinity[(size_t)j] = hs[(size_t)(i * P + j)];
+        }
+        l.lastPoint = {hl[(size_t)(3 * i)], hl[(size_t)(3 * i + 1)], hl[(size_t)(3 * i + 2)]};
+    }
+    return lines;
+}
+
+}  // namespace
+
+// ---- data model setters (MPASOGrid.cpp:82-188, MPASOSolution.cpp:1145-1210) ----
+void MPASOGrid::setGridAttribute(GridAttributeType type, int val) {
+    switch (type) {
+        case GridAttributeType::kCellSize: mCellsSize = val; break;
+        case GridAttributeType::kEdgeSize: mEdgesSize = val; break;
+        case GridAttributeType::kVertexSize: mVertexSize = val; break;
+        case GridAttributeType::kMaxEdgesSize: mMaxEdgesSize = val; break;
+        case GridAttributeType::kVertLevels: mVertLevels = val; break;
+        case GridAttributeType::kVertLevelsP1: mVertLevelsP1 = val; break;
+        default: Error("[MPASOGrid]::Invalid GridAttributeType"); break;
+    }
+}
+void MPASOGrid::setGridAttributesVec3(GridAttributeType type, const std::vector<vec3>& vec) {
+    switch (type) {
+        case GridAttributeType::kVertexCoord: vertexCoord_vec = vec; break;
+        case GridAttributeType::kCellCoord: cellCoord_vec = vec; break;
+        case GridAttributeType::kEdgeCoord: edgeCoord_vec = vec; break;
+        default: std::cout << "Error: Invalid GridAttributeType" << std::endl;
+    }
+}
+void MPASOGrid::setGridAttributesVec2(GridAttributeType type, const std::vector<vec2>& vec) {
+    if (type == GridAttributeType::kVertexLatLon) vertexLatLon_vec = vec;
+    else std::cout << "Error: Invalid GridAttributeType" << std::endl;
+}
+void MPASOGrid::setGridAttributesInt(GridAttributeType type, const std::vector<size_t>& vec) {
+    switch (type) {
+        case GridAttributeType::kVerticesOnCell: verticesOnCell_vec = vec; break;
+        case GridAttributeType::kVerticesOnEdge: verticesOnEdge_vec = vec; break;
+        case GridAttributeType::kCellsOnVertex: cellsOnVertex_vec = vec; break;
+        case GridAttributeType::kCellsOnCell: cellsOnCell_vec = vec; break;
+        case GridAttributeType::kNumberVertexOnCell: numberVertexOnCell_vec = vec; break;
+        case GridAttributeType::kCellsOnEdge: cellsOnEdge_vec = vec; break;
+        case GridAttributeType::kEdgesOnCell: edgesOnCell_vec = vec; break;
+        default: std::cout << "Error: Invalid GridAttributeType" << std::endl;
+    }
+}
+void MPASOGrid::setGridAttributesFloat(GridAttributeType type, const std::vector<float>& vec) {
+    if (type == GridAttributeType::kCellWeight) cellWeight_vec = vec;
+    else std::cout << "Error: Invalid GridAttributeType" << std::endl;
+}
+bool MPASOGrid::checkAttribute() const {  // MPASOGrid.cpp:516-598
+    return mCellsSize != 0 && mVertexSize != 0 && mMaxEdgesSize != 0 && mVertLevels != 0 && mVertLevelsP1 != 0 &&
+           !cellCoord_vec.empty() && !vertexCoord_vec.empty() && !verticesOnCell_vec.empty() &&
+           !cellsOnVertex_vec.empty() && !cellsOnCell_vec.empty() && !numberVertexOnCell_vec.empty();
+}
+
+void MPASOSolution::setAttribute(GridAttributeType type, int val) {
+    switch (type) {
+        case GridAttributeType::kCellSize: mCellsSize = val; break;
+        case GridAttributeType::kEdgeSize: mEdgesSize = val; break;
+        case GridAttributeType::kVertexSize: mVertexSize = val; break;
+        case GridAttributeType::kMaxEdgesSize: mMaxEdgesSize = val; break;
+        case GridAttributeType::kVertLevels: mVertLevels = val; break;
+        case GridAttributeType::kVertLevelsP1: mVertLevelsP1 = val; break;
+        default: std::cerr << "[Error]: Invalid GridAttributeType" << std::endl; break;
+    }
+}
+void MPASOSolution::setAttributesDouble(AttributeType type, const std::vector<double>& vec) {
+    switch (type) {
+        case AttributeType::kZTop: cellZTop_vec = vec; break;
+        case AttributeType::kLayerThickness: cellLayerThickness_vec = vec; break;
+        case AttributeType::kBottomDepth: cellBottomDepth_vec = vec; break;
+        case AttributeType::kZonalVelocity: cellZonalVelocity_vec = vec; break;
+        case AttributeType::kMeridionalVelocity: cellMeridionalVelocity_vec = vec; break;
+        case AttributeType::kNormalVelocity: cellNormalVelocity_vec = vec; break;
+        default: std::cerr << "[Error]: Invalid AttributeType" << std::endl; break;
+    }
+}
+void MPASOSolution::setAttributesVec3(AttributeType type, const std::vector<vec3>& vec) {
+    if (type == AttributeType::kVelocity) cellCenterVelocity_vec = vec;
+    else std::cerr << "[Error]: Invalid AttributeType" << std::endl;
+}
+bool MPASOSolution::checkAttribute() const {  // MPASOSolution.cpp:1212-1232
+    if (cellZTop_vec.empty() && cellLayerThickness_vec.empty()) {
+        std::cerr << "[MPASOSolution]::Error: Invalid ZTop Attribute" << std::endl;
+        return false;
+    }
+    return true;
+}
+
+// ---- public API (MOPS.cpp) -------------------------------------------------
+void MOPS_Init(const char* device) {
+    (void)device;
+    g_app.release();
+    g_app = App();
+    hipDeviceProp_t prop{};
+    int dev = 0;
+    if (hipGetDevice(&dev) == hipSuccess && hipGetDeviceProperties(&prop, dev) == hipSuccess)
+        std::cout << " [ system information ]\nDevice selected : " << prop.name << " (" << prop.gcnArchName
+                  << ", HIP engine)\n";
+    g_app.grid = std::make_shared<MPASOGrid>();
+}
+
+void MOPS_Begin() { g_app.state = State::Configuring; }
+
+void MOPS_AddGridMesh(std::shared_ptr<MPASOGrid> grid) {
+    ScopedTimer t("Preprocessing::addGrid", "Preprocessing");
+    g_app.grid = std::move(grid);
+}
+
+void MOPS_AddAttribute(int solID, std::shared_ptr<MPASOSolution> sol) {
+    ScopedTimer t("Preprocessing::addSol", "Preprocessing");
+    if (g_app.sols.count(solID)) return;  // MOPSApp.cpp:82-87
+    auto& g = *g_app.grid;
+    sol->mCellsSize = g.mCellsSize;       // :92-98
+    sol->mEdgesSize = g.mEdgesSize;
+    sol->mMaxEdgesSize = g.mMaxEdgesSize;
+    sol->mVertexSize = g.mVertexSize;
+    g.mVertLevels = sol->mVertLevels;
+    g.mVertLevelsP1 = sol->mVertLevelsP1;
+    g_app.sols[solID] = std::move(sol);
+}
+
+void MOPS_End() {
+    if (g_app.state != State::Configuring) {  // MOPS.cpp:31-46
+        std::cerr << " [ MOPS is not configuring ]\n";
+        std::exit(1);
+    }
+    bool ok = g_app.grid && g_app.grid->checkAttribute();
+    for (auto& kv : g_app.sols) ok = ok && kv.second && kv.second->checkAttribute();
+    if (!ok) {
+        std::cerr << " [ MOPS is not configured ]\n";
+        std::exit(1);
+    }
+    g_app.state = State::Ready;
+    ScopedTimer t("Preprocessing::upload", "Preprocessing");
+    const auto& g = *g_app.grid;
+    mops_mesh_desc d{};
+    d.n_cells = g.mCellsSize;
+    d.n_vertices = g.mVertexSize;
+    d.max_edges = g.mMaxEdgesSize;
+    d.n_vert_levels = g.mVertLevels;
+    d.h_n_edges_on_cell = reinterpret_cast<const uint64_t*>(g.numberVertexOnCell_vec.data());
+    d.h_vertices_on_cell = reinterpret_cast<const uint64_t*>(g.verticesOnCell_vec.data());
+    d.h_cells_on_cell = reinterpret_cast<const uint64_t*>(g.cellsOnCell_vec.data());
+    d.h_cells_on_vertex = reinterpret_cast<const uint64_t*>(g.cellsOnVertex_vec.data());
+    d.h_cell_coord = reinterpret_cast<const double*>(g.cellCoord_vec.data());
+    d.h_vertex_coord = reinterpret_cast<const double*>(g.vertexCoord_vec.data());
+    g_app.release();
+    check(mops_mesh_create(&d, nullptr, &g_app.mesh), "mops_mesh_create");
+    for (auto& kv : g_app.sols) g_app.fields[kv.first] = make_field(*kv.second);
+    if (!g_app.fields.empty()) g_app.front = g_app.fields.begin()->second;  // addField: first map entry
+}
+
+void MOPS_ActiveAttribute(int t1, std::optional<int> t2) {  // MOPSApp.cpp:145-169
+    g_app.front = g_app.back = nullptr;
+    auto it = g_app.fields.find(t1);
+    if (it == g_app.fields.end()) {
+        Error("[MOPSApp]::activeAttribute: solID %d not found", t1);
+        return;
+    }
+    if (t2.has_value()) {
+        auto it2 = g_app.fields.find(t2.value());
+        if (it2 == g_app.fields.end()) {
+            Error("[MOPSApp]::activeAttribute: solID %d not found", t2.value());
+            return;
+        }
+        g_app.back = it2->second;
+    }
+    g_app.front = it->second;
+}
+
+std::vector<TrajectoryLine> MOPS_RunStreamLine(TrajectorySettings* config, std::vector<CartesianCoord>& sample_points) {
+    ScopedTimer t("GPUKernel::StreamLine", "GPUKernel");
+    return run(config, sample_points, false, "MI355X::StreamLine");
+}
+
+std::vector<TrajectoryLine> MOPS_RunPathLine(TrajectorySettings* config, std::vector<CartesianCoord>& sample_points) {
+    ScopedTimer t("GPUKernel::PathLine", "GPUKernel");
+    if (g_app.front == nullptr || g_app.back == nullptr) {  // MOPSApp.cpp:259-271
+        Error("[MOPSApp]::Sol_Front or Sol_Back is nullptr, please activeAttribute first");
+        std::exit(-1);
+    }
+    auto lines = run(config, sample_points, true, "MI355X::PathLine");
+    for (size_t i = 0; i < sample_points.size() && i < lines.size(); ++i)  // :287-290
+        sample_points[i] = lines[i].lastPoint;
+    return lines;
+}
+
+void MOPS_GenerateSamplePoints(SamplingSettings* config, std::vector<CartesianCoord>& points) {
+    if (config->isAtCellCenter()) {  // MOPSApp::generateSamplePointsAtCenter
+        for (const auto& p : g_app.grid->cellCoord_vec) points.push_back(p);
+        return;
+    }
+    // MPASOVisualizer::GenerateSamplePoint (MPASOVisualizer.cpp:120-149):
+    // exclusive upper bounds, accumulated steps, r = 6371010.0f.  Like the
+    // reference, the conversion pass runs over the WHOLE vector, so points the
+    // caller passed in are re-converted too.
+    const double minLat = config->getLatitudeRange().x, maxLat = config->getLatitudeRange().y;
+    const double minLon = config->getLongitudeRange().x, maxLon = config->getLongitudeRange().y;
+    const double i_step = (maxLat - minLat) / static_cast<double>(config->getSampleRange().x - 1);
+    const double j_step = (maxLon - minLon) / static_cast<double>(config->getSampleRange().y - 1);
+    for (double i = minLat; i < maxLat; i += i_step)
+        for (double j = minLon; j < maxLon; j += j_step) points.push_back({j, i, config->getDepth()});
+    const double r = 6371010.0f;
+    for (size_t k = 0; k < points.size(); ++k) {
+        const double lat = points[k].y * (M_PI / 180.0), lon = points[k].x * (M_PI / 180.0);
+        const double ct = std::cos(lat), cp = std::cos(lon), st = std::sin(lat), sp = std::sin(lon);
+        points[k] = {r * ct * cp, r * ct * sp, r * st};
+    }
+}
+
+void MOPS_ResetTiming() { g_timing = Timing(); }
+void MOPS_PrintTimingSummary() {
+    std::cout << "==== MOPS timing summary (ms) ====\n";
+    for (auto& kv : g_timing.by_category) std::cout << "  " << kv.first << ": " << kv.second << "\n";
+}
+void MOPS_PrintTimingDetailed() {
+    std::cout << "==== MOPS timing detailed (ms) ====\n";
+    for (auto& r : g_timing.records) std::cout << "  " << r.first << ": " << r.second << "\n";
+}
+double MOPS_GetCategoryTime(const char* category) {
+    auto it = g_timing.by_category.find(category ? category : "Other");
+    return it == g_timing.by_category.end() ? 0.0 : it->second;
+}
+double MOPS_GetTotalTime() {
+    double s = 0.0;
+    for (auto& kv : g_timing.by_category) s += kv.second;
+    return s;
+}
+
+std::vector<TrajectoryLine> RemoveNaNTrajectoriesAndReindex(std::vector<TrajectoryLine>& lines) {
+    std::vector<TrajectoryLine> out;
+    out.reserve(lines.size());
+    int new_id = 0;
+    for (auto& l : lines) {
+        const size_t P = l.points.size();
+        if (P == 0) continue;  // TrajectoryCommon.h:84-86
+        l.velocity.resize(P, CartesianCoord{0.0, 0.0, 0.0});
+        l.temperature.resize(P, 0.0);
+        l.salinity.resize(P, 0.0);
+        double *dp = nullptr, *dv = nullptr, *dt = nullptr, *ds = nullptr, *dl = nullptr;
+        check(hipMalloc(&dp, P * 24) == hipSuccess && hipMalloc(&dv, P * 24) == hipSuccess &&
+                      hipMalloc(&dt, P * 8) == hipSuccess && hipMalloc(&ds, P * 8) == hipSuccess &&
+                      hipMalloc(&dl, 24) == hipSuccess
+                  ? MOPS_OK
+                  : MOPS_ERR_HIP,
+              "hipMalloc");
+        (void)hipMemcpy(dp, l.points.data(), P * 24, hipMemcpyHostToDevice);
+        (void)hipMemcpy(dv, l.velocity.data(), P * 24, hipMemcpyHostToDevice);
+        (void)hipMemcpy(dt, l.temperature.data(), P * 8, hipMemcpyHostToDevice);
+        (void)hipMemcpy(ds, l.salinity.data(), P * 8, hipMemcpyHostToDevice);
+        const mops_status st = mops_remove_nan_lines(1, (int64_t)P, dp, dv, dt, ds, dl, nullptr);
+        (void)hipMemcpy(l.points.data(), dp, P * 24, hipMemcpyDeviceToHost);
+        (void)hipMemcpy(l.velocity.data(), dv, P * 24, hipMemcpyDeviceToHost);
+        (void)hipMemcpy(l.temperature.data(), dt, P * 8, hipMemcpyDeviceToHost);
+        (void)hipMemcpy(l.salinity.data(), ds, P * 8, hipMemcpyDeviceToHost);
+        (void)hipMemcpy(&l.lastPoint, dl, 24, hipMemcpyDeviceToHost);
+        (void)hipFree(dp); (void)hipFree(dv); (void)hipFree(dt); (void)hipFree(ds); (void)hipFree(dl);
+        check(st, "mops_remove_nan_lines");
+        l.lineID = new_id++;
+        out.push_back(l);
+    }
+    return out;
+}
+
+}  // namespace MOPS
