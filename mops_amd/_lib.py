@@ -68,6 +68,14 @@ def load(path: str | None = None):
     if not os.path.exists(path):
         raise MopsError(f"HIP engine library not found at {path}: run `python -c \"import __graft_entry__ as g; "
                         f"g.build()\"` (hipcc --offload-arch=gfx950) first")
+    # torch ships its own libamdhip64 (SONAME libamdhip64.so.7, but NEEDED as
+    # "libamdhip64.so"): load it first so the engine binds to the same HIP
+    # runtime instead of pulling a second copy from /opt/rocm -- two runtimes
+    # in one process make the second one report "no ROCm-capable device".
+    try:
+        import torch  # noqa: F401
+    except ImportError:
+        pass
     lib = C.CDLL(path)
     P, I64, I32 = C.c_void_p, C.c_int64, C.c_int32
     st = C.c_int
