@@ -9,6 +9,9 @@ the rank's particle shard: seed location, 720 integration steps in 24
 record segments and -- for N > 1 -- an RCCL all-gather of each record slab
 over xGMI on a side stream, overlapped with the next segment's kernel.
 
+``--config 3``: BASELINE configs[2] -- 1e7 particles/GPU, layer 10, dt 60 s,
+7-day pathline as 7 chained daily snapshot pairs (mops_amd/chain.py).
+
 Inputs (mesh, fields, seeds) are resident in HBM before the timed region.
 Rank 0 prints one JSON line (driver contract).
 """
@@ -44,9 +47,39 @@ def parse():
     p.add_argument("--method", choices=["euler", "rk4"], default="euler")
     p.add_argument("--mode", choices=["streamline", "pathline"], default="streamline",
                    help="pathline: two snapshots (front/back), BASELINE config 3 shape")
+    p.add_argument("--config", type=int, choices=[2, 3], default=2,
+                   help="BASELINE.json config: 2 = 1e6-particle 1-day streamline (default); 3 = 1e7-particle "
+                        "7-day chained pathline at layer 10, dt 60 s")
+    p.add_argument("--pairs", type=int, default=7, help="config 3: snapshot pairs (days)")
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--cpu-seconds", type=float, default=12.0, help="target CPU-baseline sample length")
     return p.parse_args()
+
+
+def make_seeds(n: int, rank: int) -> np.ndarray:
+    """Uniform on |lat| < 70 deg, rejected on land; one shard per rank."""
+    from mops_amd import synth
+    seeds = synth.uniform_band_seeds(int(n * 1.25) + 64, seed=12345 + rank)
+    r = np.linalg.norm(seeds, axis=1)
+    lat = np.arcsin(seeds[:, 2] / r); lon = np.arctan2(seeds[:, 1], seeds[:, 0])
+    return seeds[~synth._land_mask(lat, lon, "continents")][:n]
+
+
+def measured_traffic(key: str, avg_kernel_s: float):
+    """Per-launch DRAM bytes from the committed PMC summary (tools/make_traffic.py), if it is for this workload."""
+    pmc_path = os.path.join(ROOT, "profiles", "pmc_traffic.json")
+    if not os.path.exists(pmc_path):
+        return None, None
+    try:
+        pm = json.load(open(pmc_path))
+        entries = pm if isinstance(pm, list) else [pm]
+        for e in entries:
+            if e.get("workload") == key:
+                t = e.get("bytes_per_launch")
+                return t, t / avg_kernel_s / 1e9
+    except Exception:
+        pass
+    return None, None
 
 
 def algorithmic_bytes_per_pstep(nv: float, L: int, S: int = 1) -> float:
@@ -54,8 +87,22 @@ def algorithmic_bytes_per_pstep(nv: float, L: int, S: int = 1) -> float:
     return (4 + 4 * nv + 4 * nv + 24 * nv + 24 * (nv + 1) + S * (8 * nv * L + 2 * 24 * nv + 2 * 8 * nv) + 32)
 
 
+CONFIG3 = dict(mode="pathline", particles=10_000_000, dt=60, duration=86400, record=3600, method="euler")
+
+
+def layer_mid_depth(mesh, layer: int = 10) -> float:
+    """"fixed layer 10" = mid-depth of 0-based layer 10."""
+    return 0.5 * (float(mesh.refBottomDepth[layer - 1]) + float(mesh.refBottomDepth[layer]))
+
+
 def main():
     args = parse()
+    if args.config == 3:  # config-3 values for every option left at its config-2 default
+        d = vars(argparse.Namespace(mode="streamline", particles=1_000_000, dt=120, duration=86400, record=3600,
+                                    method="euler"))
+        for k, v in CONFIG3.items():
+            if getattr(args, k) == d[k]:
+                setattr(args, k, v)
     import torch
     import torch.distributed as dist
 
@@ -71,21 +118,20 @@ def main():
     from mops_amd.engine import DeviceField, DeviceMesh, ParticleSet, TrajectoryConfig
 
     mesh = synth.make_mesh(args.freq, n_levels=args.levels)
+    if args.config == 3:
+        args.depth = layer_mid_depth(mesh, 10)
+        return main_chain(args, mesh, dev, world, rank)
     snap = synth.make_snapshot(mesh, timestep=0)
     dmesh = DeviceMesh.from_mesh(mesh)
     dfield = DeviceField.from_snapshot(dmesh, snap)
     pathline = args.mode == "pathline"
     dback = DeviceField.from_snapshot(dmesh, synth.make_snapshot(mesh, timestep=1, phase=0.35)) if pathline else None
-    # seeds: uniform on |lat| < 70 deg, rejected on land, one shard per rank
-    rng_seed = 12345 + rank
-    seeds = synth.uniform_band_seeds(int(args.particles * 1.25) + 64, seed=rng_seed)
-    r = np.linalg.norm(seeds, axis=1)
-    lat = np.arcsin(seeds[:, 2] / r); lon = np.arctan2(seeds[:, 1], seeds[:, 0])
-    seeds = seeds[~synth._land_mask(lat, lon, "continents")][: args.particles]
+    seeds = make_seeds(args.particles, rank)
     n = seeds.shape[0]
     cfg = TrajectoryConfig(deltaT=args.dt, simulationDuration=args.duration, recordT=args.record, depth=args.depth,
                            method=1 if args.method == "euler" else 0)
     ps = ParticleSet(dmesh, seeds, args.depth, cfg, device=dev)
+    seed_cells = ps.cell.cpu().numpy()
     period = ps.record_period(pathline=pathline)
     n_steps = cfg.n_steps
     bounds = list(range(0, n_steps, period)) + [n_steps]
@@ -158,22 +204,12 @@ def main():
     B = algorithmic_bytes_per_pstep(nv_mean, mesh.nVertLevels, 2 if pathline else 1)
     psteps_per_launch = attempted / len(segments)
     achieved = B * psteps_per_launch / avg_kernel_s / 1e9
-    traffic = None
-    measured = None
-    pmc_path = os.path.join(ROOT, "profiles", "pmc_traffic.json")
-    if os.path.exists(pmc_path):
-        try:
-            pm = json.load(open(pmc_path))
-            if pm.get("workload") == f"ec30to60_{args.mode}_{args.method}_{args.particles}":
-                traffic = pm.get("bytes_per_launch")
-                measured = traffic / avg_kernel_s / 1e9
-        except Exception:
-            traffic = None
+    traffic, measured = measured_traffic(f"ec30to60_{args.mode}_{args.method}_{args.particles}", avg_kernel_s)
 
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         back_snap = synth.make_snapshot(mesh, timestep=1, phase=0.35) if pathline else None
-        cpu = cpu_baseline(mesh, snap, back_snap, seeds, ps.cell.cpu().numpy(), args, n_steps)
+        cpu = cpu_baseline(mesh, snap, back_snap, seeds, seed_cells, args, n_steps)
 
     if rank == 0:
         line = {
@@ -222,6 +258,119 @@ def main():
         print(json.dumps(line))
     if world > 1:
         dist.destroy_process_group()
+
+
+def main_chain(args, mesh, dev, world, rank):
+    """BASELINE config 3: 1e7 particles/GPU, "layer 10", dt 60 s, 7-day pathline as 7 chained daily snapshot
+    pairs (MOPSPathline.run semantics, mops_amd/chain.py).  All 8 derived snapshots are resident in HBM before
+    the timed region; one bench step = the whole 7-day chain (seed locate per pair, 10 080 steps, per-pair line
+    assembly on device, an RCCL all-gather of each pair's continuation points when N > 1)."""
+    import torch
+    import torch.distributed as dist
+    from mops_amd import synth
+    from mops_amd.chain import PathlineChain
+    from mops_amd.engine import DeviceField, DeviceMesh
+
+    n_snap = args.pairs + 1
+    snaps = [synth.make_snapshot(mesh, timestep=t, phase=0.35 * t) for t in range(n_snap)]
+    dmesh = DeviceMesh.from_mesh(mesh)
+    fields = [DeviceField.from_snapshot(dmesh, s) for s in snaps]
+    seeds = make_seeds(args.particles, rank)
+    n = seeds.shape[0]
+    chain = PathlineChain(dmesh, lambda i, stream: fields[i], n_snap, gap_seconds=args.duration, device=dev,
+                          own_fields=False)
+    compute = torch.cuda.Stream(dev)
+    comm = torch.cuda.Stream(dev)
+    gathered = torch.empty((world, n, 3), dtype=torch.float64, device=dev) if world > 1 else None
+    timing = []
+
+    def on_pair(p, last):
+        if world > 1:  # checkpoint: every rank gets the continuation points of all shards
+            done = torch.cuda.Event(); done.record(compute)
+            comm.wait_event(done)
+            last.record_stream(comm)
+            with torch.cuda.stream(comm):
+                dist.all_gather_into_tensor(gathered.view(-1), last.view(-1))
+
+    def one_call(timed):
+        res = chain.run(seeds, depth=args.depth, method=1 if args.method == "euler" else 0, delta_t=args.dt,
+                        record_t=args.record, keep_lines=False, compute_stream=compute, on_pair=on_pair,
+                        timing=timing if timed else None)
+        compute.synchronize(); comm.synchronize()
+        return res
+
+    for _ in range(args.warmup):
+        one_call(False)
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    attempted = 0
+    for _ in range(args.steps):
+        attempted += int(one_call(True)["attempted"].item())
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    kms = [a.elapsed_time(b) for (a, b) in timing]
+    avg_kernel_s = (sum(kms) / len(kms)) / 1e3
+    stats = torch.tensor([elapsed, float(attempted), float(n)], dtype=torch.float64, device=dev)
+    if world > 1:
+        mx = stats.clone(); dist.all_reduce(mx, op=dist.ReduceOp.MAX)
+        sm = stats.clone(); dist.all_reduce(sm, op=dist.ReduceOp.SUM)
+        elapsed, attempted_all, n_all = mx[0].item(), sm[1].item(), sm[2].item()
+    else:
+        attempted_all, n_all = float(attempted), float(n)
+    n_steps = args.pairs * (args.duration // args.dt)
+    value = attempted_all / elapsed
+    nv_mean = float(np.mean(mesh.nEdgesOnCell.astype(np.float64)))
+    B = algorithmic_bytes_per_pstep(nv_mean, mesh.nVertLevels, 2)
+    launches_per_call = len(timing) / args.steps
+    psteps_per_launch = attempted / args.steps / launches_per_call
+    achieved = B * psteps_per_launch / avg_kernel_s / 1e9
+    traffic, measured = measured_traffic(f"ec30to60_chain_{args.method}_{args.particles}", avg_kernel_s)
+    cpu = None
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        seed_cells = dmesh_locate_host(dmesh, seeds, dev)
+        cpu = cpu_baseline(mesh, snaps[0], snaps[1], seeds, seed_cells, args, args.duration // args.dt)
+    if rank == 0:
+        print(json.dumps({
+            "metric": "particle-steps/sec", "value": value, "unit": "particle-steps/s", "n_gpus": world,
+            "steps": args.steps, "warmup": args.warmup, "ms_per_step": elapsed / args.steps * 1e3,
+            "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "f64",
+            "data": "synthetic (icosahedral-dual Voronoi mesh, analytic flow phase-shifted per daily snapshot)",
+            "config": {
+                "workload": (f"EC30to60-class chained pathline (BASELINE config 3), {n:.0e} particles/GPU, layer 10 "
+                             f"({args.depth:.1f} m), dt {args.dt} s, {args.pairs} days = {args.pairs} daily pairs"),
+                "cells": mesh.nCells, "vertices": mesh.nVertices, "levels": mesh.nVertLevels,
+                "particles_per_gpu": n, "particles_total": int(n_all), "integration_steps": n_steps,
+                "records_per_pair": args.duration // args.record, "method": args.method,
+                "parallelism": f"particle-shard x{world}",
+                "record_gather": "rccl all_gather of continuation points per pair" if world > 1 else "none"},
+            "nominal_particle_steps_per_call": n_all * n_steps,
+            "attempted_particle_steps_per_call": attempted_all / args.steps,
+            "roofline": {
+                "bound": "hbm", "achieved": achieved, "peak": PEAK_HBM_GBS, "unit": "GB/s",
+                "frac": achieved / PEAK_HBM_GBS, "traffic": traffic,
+                "kernel": f"traj_kernel<7,true,{str(args.method == 'euler').lower()}> (pathline {args.method})",
+                "algorithmic_bytes_per_particle_step": B,
+                "algorithmic_bytes_note": "SURVEY.md 8(d) model (S=2); see measured_* for DRAM traffic",
+                "measured_hbm_gbs": measured,
+                "measured_frac": (measured / PEAK_HBM_GBS) if measured else None,
+                "particle_steps_per_launch": psteps_per_launch, "avg_launch_ms": avg_kernel_s * 1e3},
+            "cpu_baseline": cpu,
+        }))
+    if world > 1:
+        dist.destroy_process_group()
+
+
+def dmesh_locate_host(dmesh, seeds, dev):
+    import torch
+    s = torch.as_tensor(np.ascontiguousarray(seeds, dtype=np.float64), device=dev)
+    c = torch.empty((s.shape[0],), dtype=torch.int32, device=dev)
+    dmesh.locate(s.data_ptr(), c.data_ptr(), int(s.shape[0]))
+    torch.cuda.synchronize()
+    return c.cpu().numpy()
 
 
 def cpu_baseline(mesh, snap, back_snap, seeds, cells, args, n_steps):

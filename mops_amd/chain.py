@@ -1,0 +1,140 @@
+"""Snapshot-pair chaining for long pathlines, device resident.
+
+Host-side mirror of the reference's pair loop -- ``MOPSPathline.run``
+(tutorial/pyMOPSAPI.py:1396-1531) and tutorial/pathLine.cpp:244-309 --
+with the MI355X-specific change that nothing leaves HBM between pairs:
+
+* snapshot i+2's derived field is built on a side stream while pair i runs,
+  and a field is freed as soon as no pair needs it (at most 3 resident);
+* the continuation seeds (each pair's ``lastPoint``), the per-particle
+  depths and the concatenated lines stay device tensors.
+
+Per-pair semantics are the reference's:
+* pair p runs a PathLine with front = snapshot p, back = snapshot p+1 and
+  ``simulationDuration`` = the snapshot gap;
+* seeds: pair 0 uses the given seeds, later pairs the previous pair's
+  ``lastPoint`` if ``follow_last`` else the original seeds again (:1446-1459);
+* depth: constant mode re-applies ``cfg.depth`` every pair (``cfg.depth =
+  self._depth``, :1470); per-particle mode carries
+  ``clip(EARTH_RADIUS_M - |lastPoint|, 0)`` as float32 (:1462-1467, 1486-1491);
+* lines: pair 0's lines whole, later pairs without their first sample
+  (:1500-1516); ``lastPoint`` = the last pair's.
+"""
+from __future__ import annotations
+
+import numpy as np
+
+from . import _lib as L
+from .engine import DeviceField, DeviceMesh, ParticleSet, TrajectoryConfig
+
+EARTH_RADIUS_M = 6_371_000.0  # pyMOPSAPI.py:46
+
+
+class PathlineChain:
+    def __init__(self, mesh: DeviceMesh, make_field, n_snapshots: int, gap_seconds: int, device=None,
+                 own_fields: bool = True):
+        """``make_field(i, stream) -> DeviceField`` builds snapshot i's field on ``stream``.
+        With ``own_fields`` False the fields are the caller's (e.g. all resident
+        before a timed region) and are neither freed nor rebuilt here."""
+        if n_snapshots < 2:
+            raise ValueError("a pathline chain needs at least two snapshots")
+        self.mesh = mesh
+        self.make_field = make_field
+        self.n_snapshots = int(n_snapshots)
+        self.gap = int(gap_seconds)
+        self.device = device
+        self.own_fields = own_fields
+
+    def run(self, seeds, depth: float, particle_depths=None, method: int = L.MOPS_EULER, delta_t: int = 60,
+            record_t: int = 360, direction: int = L.MOPS_FORWARD, follow_last: bool = True, keep_lines: bool = True,
+            compute_stream=None, on_pair=None, timing=None):
+        """Run all pairs; returns device tensors {points, velocity, temperature,
+        salinity, lastPoint, death_step (of the last pair)} when ``keep_lines``,
+        else only lastPoint/death_step.  ``on_pair(p, last)`` is called after pair p
+        is enqueued (timing / record gathers); ``timing`` (a list) receives an
+        (start, end) HIP event pair around every trajectory launch.
+        ``attempted`` in the result counts particle-steps whose velocity
+        evaluation ran, summed over pairs (device scalar)."""
+        import torch
+        dev = self.device or torch.device("cuda", torch.cuda.current_device())
+        cs = compute_stream or torch.cuda.current_stream(dev)
+        side = torch.cuda.Stream(device=dev)
+        cfg = TrajectoryConfig(deltaT=int(delta_t), simulationDuration=self.gap, recordT=int(record_t),
+                               depth=float(np.float32(depth)), direction=int(direction), method=int(method))
+        if cfg.n_steps <= 0 or cfg.n_records <= 0:
+            raise ValueError("invalid trajectory settings for a pair (deltaT/recordT vs the snapshot gap)")
+        seeds0 = torch.as_tensor(np.ascontiguousarray(seeds, dtype=np.float64).reshape(-1, 3), device=dev)
+        n = int(seeds0.shape[0])
+        per_particle = particle_depths is not None and len(particle_depths) == n
+        pdep = (torch.as_tensor(np.asarray(particle_depths, dtype=np.float32), device=dev) if per_particle else None)
+
+        fields = {}
+        with torch.cuda.stream(cs):
+            fields[0] = self.make_field(0, cs.cuda_stream)
+            fields[1] = self.make_field(1, cs.cuda_stream)
+            ps = ParticleSet(self.mesh, seeds0.cpu().numpy(), cfg.depth, cfg, device=dev)
+        period = ps.record_period(pathline=True)
+        pts_acc, vel_acc, tmp_acc, sal_acc = [], [], [], []
+        last = None
+        attempted = torch.zeros((), dtype=torch.int64, device=dev)
+        for p in range(self.n_snapshots - 1):
+            with torch.cuda.stream(cs):
+                if p == 0 or not follow_last:
+                    s = seeds0
+                else:
+                    s = last
+                if per_particle:
+                    if p > 0 and follow_last:
+                        # np.linalg.norm(axis=1) order: sqrt((x*x + y*y) + z*z)
+                        r = torch.sqrt((s[:, 0] * s[:, 0] + s[:, 1] * s[:, 1]) + s[:, 2] * s[:, 2])
+                        pdep = torch.clamp(EARTH_RADIUS_M - r, min=0.0).to(torch.float32)
+                    d = pdep
+                else:
+                    d = cfg.depth
+                ps.reseed(s, d, stream=cs.cuda_stream)
+                front, back = fields[p], fields[p + 1]
+                for s0 in range(0, cfg.n_steps, period):
+                    if timing is not None:
+                        e0 = torch.cuda.Event(enable_timing=True); e1 = torch.cuda.Event(enable_timing=True)
+                        e0.record(cs)
+                    ps.advance(front, back, s0, min(s0 + period, cfg.n_steps), stream=cs.cuda_stream)
+                    if timing is not None:
+                        e1.record(cs)
+                        timing.append((e0, e1))
+                out = ps.finalize(pathline=True, stream=cs.cuda_stream)
+                dth = ps.death.to(torch.int64)
+                attempted += torch.where(dth < 0, torch.full_like(dth, cfg.n_steps), dth + 1).sum()
+                last = out["lastPoint"].clone()
+                if keep_lines:
+                    sl = slice(None) if p == 0 else slice(1, None)
+                    pts_acc.append(out["points"][:, sl]); vel_acc.append(out["velocity"][:, sl])
+                    tmp_acc.append(out["temperature"][:, sl]); sal_acc.append(out["salinity"][:, sl])
+            if on_pair is not None:
+                on_pair(p, last)
+            # overlap: build the field pair p+1 will need while pair p computes
+            if p + 2 < self.n_snapshots:
+                if self.own_fields:
+                    with torch.cuda.stream(side):
+                        fields[p + 2] = self.make_field(p + 2, side.cuda_stream)
+                    cs.wait_stream(side)
+                else:
+                    fields[p + 2] = self.make_field(p + 2, cs.cuda_stream)
+            done = fields.pop(p)
+            if self.own_fields:
+                cs.synchronize()  # pair p finished with `done` before it is freed
+                done.close()
+        if self.own_fields:
+            for f in fields.values():
+                f.close()
+        res = dict(lastPoint=last, death_step=ps.death.clone(), attempted=attempted)
+        if keep_lines:
+            res.update(points=torch.cat(pts_acc, 1), velocity=torch.cat(vel_acc, 1), temperature=torch.cat(tmp_acc, 1),
+                       salinity=torch.cat(sal_acc, 1))
+        return res
+
+
+def snapshot_field_factory(mesh: DeviceMesh, make_snapshot):
+    """``make_field`` for PathlineChain from a host ``make_snapshot(i)`` (raw MPASOSolution arrays)."""
+    def make(i, stream):
+        return DeviceField.from_snapshot(mesh, make_snapshot(i), stream=stream)
+    return make

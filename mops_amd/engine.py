@@ -236,6 +236,26 @@ class ParticleSet:
         self.death.fill_(-1)
         self.records.zero_()
 
+    def reseed(self, seeds, depth, stream=None):
+        """Start a new run from device-resident seeds [n,3] (f64) and depth (scalar
+        or [n] f32): state <- seeds, death cleared, records zeroed, seed cells
+        located (the reference's calcInWhichCells per run) and re-ordered."""
+        torch = self.torch
+        s = seeds.reshape(-1, 3)
+        if int(s.shape[0]) != self.n:
+            raise ValueError("reseed: particle count changed")
+        self.seeds.copy_(s)
+        self.x.copy_(s[:, 0]); self.y.copy_(s[:, 1]); self.z.copy_(s[:, 2])
+        if isinstance(depth, torch.Tensor):
+            self.depth.copy_(depth.to(torch.float32))
+        else:
+            self.depth.fill_(float(np.float32(depth)))
+        self.death.fill_(-1)
+        self.records.zero_()
+        h = stream if stream is not None else torch.cuda.current_stream(self.seeds.device).cuda_stream
+        self.mesh.locate(self.seeds.data_ptr(), self.cell.data_ptr(), self.n, stream=h)
+        self.reorder(stream=h)
+
     def particles(self) -> L.Particles:
         return L.Particles(self.n, self.x.data_ptr(), self.y.data_ptr(), self.z.data_ptr(), self.depth.data_ptr(),
                            self.cell.data_ptr(), self.death.data_ptr(),
