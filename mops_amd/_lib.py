@@ -21,6 +21,8 @@ EXPORTED = (
     "mops_locate_cells", "mops_order_particles",
     "mops_traj_num_records", "mops_traj_num_steps", "mops_traj_advance", "mops_traj_finalize",
     "mops_remove_nan_lines", "mops_run_trajectories",
+    # include/mops_io.h
+    "mops_lines_geo", "mops_write_lines_vtp", "mops_write_lines_txt", "mops_write_pathline_binary",
 )
 
 MOPS_OK, MOPS_ERR_INVALID, MOPS_ERR_HIP, MOPS_ERR_UNSUPPORTED = 0, -1, -2, -3
@@ -88,6 +90,12 @@ def load(path: str | None = None):
     lib.mops_field_create_derived.argtypes = [P, P, P, P, P, P]; lib.mops_field_create_derived.restype = st
     lib.mops_field_export.argtypes = [P, P, P, P, P]; lib.mops_field_export.restype = st
     lib.mops_cell_to_vertex_attr.argtypes = [P, P, P, P]; lib.mops_cell_to_vertex_attr.restype = st
+    lib.mops_lines_geo.argtypes = [I64, I64, P, P, P, P]; lib.mops_lines_geo.restype = st
+    lib.mops_write_lines_vtp.argtypes = [C.c_char_p, I64, I64, P, P, P, C.c_int]
+    lib.mops_write_lines_vtp.restype = st
+    lib.mops_write_lines_txt.argtypes = [C.c_char_p, I64, I64, P, P]; lib.mops_write_lines_txt.restype = st
+    lib.mops_write_pathline_binary.argtypes = [C.c_char_p, I64, I64, P, P, P, P, C.c_int, C.c_int]
+    lib.mops_write_pathline_binary.restype = st
     lib.mops_field_destroy.argtypes = [P]; lib.mops_field_destroy.restype = None
     lib.mops_field_bytes.argtypes = [P]; lib.mops_field_bytes.restype = I64
     lib.mops_locate_cells.argtypes = [P, I64, P, P, P]; lib.mops_locate_cells.restype = st

@@ -35,6 +35,7 @@
 #include <string>
 #include <vector>
 
+#include "mops_io.h"
 #include "mops_traj.h"
 
 #define MOPS_ABI_VERSION 1
@@ -78,6 +79,7 @@ struct mops_mesh {
     int* d_cov = nullptr;        // [V][3] cellsOnVertex 0-based, -1 = missing (boundary)
     // seed-location bucket index
     double bucket_h = 0.0, bucket_origin = 0.0;
+    int origin_cell = -1;  // exact nearest centre to (0,0,0) (locate_kernel's tie rule)
     uint64_t* d_bkeys = nullptr;  // sorted bucket keys [C]
     int* d_bcells = nullptr;      // cell ids in key order [C]
     uint64_t* d_cell_key = nullptr;  // Morton key of each cell centre (particle locality order)
@@ -809,6 +811,25 @@ __global__ void __launch_bounds__(kTrajBlock, (TrajWaves<PATH, EULER>::value)) t
 // ===========================================================================
 // output assembly: FinalizeTrajectoryLines[WithAttrs] + RemoveNaN
 // ===========================================================================
+// xyz -> {lat, lon (deg), r, |v|} per line point (GeoConverter::convertXYZToLatLonDegree,
+// VTKFileManager.hpp:352-395) -- the streaming half of the output writers
+__global__ void lines_geo_kernel(int64_t m, const double* __restrict__ pts, const double* __restrict__ vel,
+                                 double* __restrict__ geo) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= m) return;
+    const double x = pts[3 * i], y = pts[3 * i + 1], z = pts[3 * i + 2];
+    const double r = sqrt(x * x + y * y + z * z);
+    const double theta = asin(z / r), phi = atan2(y, x);
+    double vm = 0.0;
+    if (vel) {
+        const double vx = vel[3 * i], vy = vel[3 * i + 1], vz = vel[3 * i + 2];
+        vm = sqrt(vx * vx + vy * vy + vz * vz);
+    }
+    double4 o;
+    o.x = theta * (180.0 / M_PI); o.y = phi * (180.0 / M_PI); o.z = r; o.w = vm;
+    reinterpret_cast<double4*>(geo)[i] = o;
+}
+
 __device__ __forceinline__ bool finite3(double a, double b, double c) { return isfinite(a) && isfinite(b) && isfinite(c); }
 
 __global__ void remove_nan_kernel(int64_t n, int64_t P, double* pts, double* vel, double* tmp, double* sal,
@@ -987,10 +1008,14 @@ __device__ __forceinline__ void consider(const double4* cxyz, int cid, double qx
 }
 
 __global__ void locate_kernel(int64_t n, const double* pts, int64_t C, const double4* cxyz, const uint64_t* keys,
-                              const int* ids, double origin, double h, int* out) {
+                              const int* ids, double origin, double h, int origin_cell, int* out) {
     const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n) return;
     const double qx = pts[3 * i], qy = pts[3 * i + 1], qz = pts[3 * i + 2];
+    // (0,0,0) is where a particle that died before its first record continues
+    // from in a pair chain (lastPoint = 0, quirk Q1); its exact answer is
+    // precomputed instead of scanning every cell
+    if (qx == 0.0 && qy == 0.0 && qz == 0.0) { out[i] = origin_cell; return; }
     double best = INFINITY;
     int bi = -1;
     const int kMaxShell = 6;
@@ -1281,6 +1306,14 @@ mops_status mops_mesh_create(const mops_mesh_desc* desc, void* stream, mops_mesh
             }
             cc[c] = make_double4(h[3 * c], h[3 * c + 1], h[3 * c + 2], rs2);
         }
+        {   // same arithmetic as locate_kernel's consider() for q = 0: d = -c, sum of squares in dim order
+            double best = INFINITY;
+            for (int64_t c = 0; c < C; ++c) {
+                double dd = 0.0;
+                dd += h[3 * c] * h[3 * c]; dd += h[3 * c + 1] * h[3 * c + 1]; dd += h[3 * c + 2] * h[3 * c + 2];
+                if (dd < best) { best = dd; m->origin_cell = (int)c; }
+            }
+        }
         if ((st = dmalloc(&m->d_cxyz, (size_t)C, &acc)) != MOPS_OK) { free_mesh(m); return st; }
         hipError_t e2 = hipMemcpyAsync(m->d_cxyz, cc.data(), C * sizeof(double4), hipMemcpyHostToDevice, s);
         if (e2 == hipSuccess) e2 = hipStreamSynchronize(s);
@@ -1482,7 +1515,7 @@ mops_status mops_locate_cells(const mops_mesh* mesh, int64_t n, const double* d_
     if (n == 0) return MOPS_OK;
     hipStream_t s = (hipStream_t)stream;
     locate_kernel<<<grid_for(n), kBlock, 0, s>>>(n, d_points, mesh->C, mesh->d_cxyz, mesh->d_bkeys, mesh->d_bcells,
-                                                 mesh->bucket_origin, mesh->bucket_h, d_cells);
+                                                 mesh->bucket_origin, mesh->bucket_h, mesh->origin_cell, d_cells);
     HIP_TRY(hipGetLastError());
     return MOPS_OK;
 }
@@ -1588,6 +1621,22 @@ mops_status mops_traj_finalize(int64_t n, int64_t K, const double* d_seeds, cons
     assemble_kernel<<<grid_for(n), kBlock, 0, s>>>(n, K, d_seeds, d_records, stride, pathline, d_points, d_vel, d_tmp,
                                                    d_sal);
     remove_nan_kernel<<<grid_for(n), kBlock, 0, s>>>(n, K + 1, d_points, d_vel, d_tmp, d_sal, d_last);
+    HIP_TRY(hipGetLastError());
+    return MOPS_OK;
+}
+
+// error hook for the host writers in mops_io.cpp (not part of the public ABI)
+__attribute__((visibility("hidden"))) mops_status mops_io_fail(mops_status st, const char* msg) {
+    return fail(st, msg ? msg : "");
+}
+
+mops_status mops_lines_geo(int64_t n, int64_t P, const double* d_points, const double* d_velocity, double* d_geo,
+                           void* stream) {
+    if (n < 0 || P < 0 || ((n * P) > 0 && (!d_points || !d_geo)))
+        return fail(MOPS_ERR_INVALID, "mops_lines_geo: invalid argument");
+    const int64_t m = n * P;
+    if (m == 0) return MOPS_OK;
+    lines_geo_kernel<<<grid_for(m), kBlock, 0, (hipStream_t)stream>>>(m, d_points, d_velocity, d_geo);
     HIP_TRY(hipGetLastError());
     return MOPS_OK;
 }

@@ -83,7 +83,9 @@ def test_locate_matches_bruteforce(gpu, dev_small, small_case, oracle_lib):
     dm, _, _ = dev_small
     pts = np.concatenate([synth.uniform_band_seeds(3000, seed=3, max_abs_lat=89.0),
                           synth.lattice_seeds(21, 21, (-60, 60), (-180, 180)),
-                          mesh.cellCoord[:50] * 1.0])           # exact cell centres
+                          mesh.cellCoord[:50] * 1.0,            # exact cell centres
+                          np.zeros((3, 3)),                      # dead-particle continuation points
+                          np.array([[1e3, -2e3, 5e2], [0.0, 0.0, 7e6]])])   # far off the sphere
     ref = oracle_lib.knn(mesh, pts)
     d = torch.as_tensor(pts, device=gpu)
     out = torch.empty(len(pts), dtype=torch.int32, device=gpu)

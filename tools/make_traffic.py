@@ -1,12 +1,14 @@
-"""profiles/pmc_traffic.json from tools/profile_round.sh output (HBM bytes per
-traj_kernel launch).  gfx950 correction (MI355X_MICROARCH.md §HBM):
-FETCH_SIZE (KiB) counts half the bytes of wide streaming reads; our reads are
-16-B-per-lane gathers, so we report 2x FETCH_SIZE (upper estimate) and keep
-the raw value beside it.  WRITE_SIZE (KiB) is taken as is."""
-import csv, glob, json, statistics, sys
+"""Merge one workload's HBM bytes per traj_kernel launch into profiles/pmc_traffic.json
+(a list of records keyed by workload) from a profile run's fetch/ and write/ passes.
+
+gfx950 correction (MI355X_MICROARCH.md §HBM): FETCH_SIZE (KiB) counts half the
+bytes of 16-B-per-lane reads, so bytes = 2 x FETCH_SIZE (the raw value is kept
+beside it); WRITE_SIZE (KiB) is taken as is.  Both are L2 memory-side counters
+(Infinity-Cache hits included)."""
+import csv, glob, json, os, statistics, sys
 out = sys.argv[1]; workload = sys.argv[2]; dst = sys.argv[3]
 def mean(counter, d):
-    v = [float(r["Counter_Value"]) for f in glob.glob(f"{out}/{d}/*counter_collection.csv")
+    v = [float(r["Counter_Value"]) for f in glob.glob(f"{out}/{d}/**/*counter_collection.csv", recursive=True)
          for r in csv.DictReader(open(f)) if "traj_kernel" in r["Kernel_Name"] and r["Counter_Name"] == counter]
     return statistics.mean(v), len(v)
 fetch, nf = mean("FETCH_SIZE", "fetch")
@@ -14,5 +16,10 @@ write, nw = mean("WRITE_SIZE", "write")
 rec = dict(workload=workload, fetch_size_kib=fetch, write_size_kib=write, dispatches=[nf, nw],
            bytes_per_launch=(2.0 * fetch + write) * 1024.0,
            note="bytes_per_launch = (2*FETCH_SIZE + WRITE_SIZE)*1024 per traj_kernel dispatch (gfx950 FETCH_SIZE correction)")
-json.dump(rec, open(dst, "w"), indent=1)
+recs = []
+if os.path.exists(dst):
+    old = json.load(open(dst))
+    recs = [r for r in (old if isinstance(old, list) else [old]) if r.get("workload") != workload]
+recs.append(rec)
+json.dump(recs, open(dst, "w"), indent=1)
 print(json.dumps(rec))
