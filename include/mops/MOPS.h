@@ -125,19 +125,32 @@ class MPASOGrid {
     std::string mCachedDataDir;
 };
 
+// SolutionID (MPASOSolution.h:12-16); timestep is value-initialised here
+struct SolutionID {
+    std::string timeStamp;
+    int timestep = 0;
+};
+
 // MPASOSolution: raw per-cell fields of one snapshot (MPASOSolution.h).
 class MPASOSolution {
   public:
     void setAttribute(GridAttributeType type, int val);
     void setAttributesDouble(AttributeType type, const std::vector<double>& vec);
     void setAttributesVec3(AttributeType type, const std::vector<vec3>& vec);
-    void setTimestep(int t) { mTimesteps = t; mID = t; }
-    int getID() const { return mID; }
+    void setTimestep(int t) { mTimesteps = t; }  // like the reference, does not touch mID
+    // 32-bit FNV-1a of "<timeStamp>_<timestep>" (MPASOSolution.h:74-86)
+    int getID() const {
+        const std::string key = mID.timeStamp + "_" + std::to_string(mID.timestep);
+        uint32_t h = 2166136261u;
+        for (unsigned char c : key) h = (h ^ c) * 16777619u;
+        return static_cast<int>(h);
+    }
     std::string getTimeStamp() const { return mTimeStamp; }
     bool checkAttribute() const;
 
     int mCellsSize = 0, mEdgesSize = 0, mMaxEdgesSize = 0, mVertexSize = 0, mTimesteps = 0, mVertLevels = 0,
-        mVertLevelsP1 = 0, mID = 0;
+        mVertLevelsP1 = 0;
+    SolutionID mID;
     std::string mTimeStamp;
     std::vector<double> cellLayerThickness_vec, cellBottomDepth_vec, cellSurfaceHeight_vec, cellZTop_vec,
         cellZonalVelocity_vec, cellMeridionalVelocity_vec, cellVertVelocity_vec, cellNormalVelocity_vec;

@@ -23,6 +23,9 @@ EXPORTED = (
     "mops_remove_nan_lines", "mops_run_trajectories",
     # include/mops_io.h
     "mops_lines_geo", "mops_write_lines_vtp", "mops_write_lines_txt", "mops_write_pathline_binary",
+    # include/mops_netcdf.h
+    "mops_nc_open", "mops_nc_close", "mops_nc_dim_len", "mops_nc_var_info", "mops_nc_read_f64", "mops_nc_read_i64",
+    "mops_nc_read_bytes",
 )
 
 MOPS_OK, MOPS_ERR_INVALID, MOPS_ERR_HIP, MOPS_ERR_UNSUPPORTED = 0, -1, -2, -3
@@ -96,6 +99,13 @@ def load(path: str | None = None):
     lib.mops_write_lines_txt.argtypes = [C.c_char_p, I64, I64, P, P]; lib.mops_write_lines_txt.restype = st
     lib.mops_write_pathline_binary.argtypes = [C.c_char_p, I64, I64, P, P, P, P, C.c_int, C.c_int]
     lib.mops_write_pathline_binary.restype = st
+    lib.mops_nc_open.argtypes = [C.c_char_p, P]; lib.mops_nc_open.restype = st
+    lib.mops_nc_close.argtypes = [P]; lib.mops_nc_close.restype = None
+    lib.mops_nc_dim_len.argtypes = [P, C.c_char_p, P]; lib.mops_nc_dim_len.restype = st
+    lib.mops_nc_var_info.argtypes = [P, C.c_char_p, P, P, P, P]; lib.mops_nc_var_info.restype = st
+    for fn in ("mops_nc_read_f64", "mops_nc_read_i64", "mops_nc_read_bytes"):
+        getattr(lib, fn).argtypes = [P, C.c_char_p, I64, P, I64]
+        getattr(lib, fn).restype = st
     lib.mops_field_destroy.argtypes = [P]; lib.mops_field_destroy.restype = None
     lib.mops_field_bytes.argtypes = [P]; lib.mops_field_bytes.restype = I64
     lib.mops_locate_cells.argtypes = [P, I64, P, P, P]; lib.mops_locate_cells.restype = st

@@ -15,9 +15,10 @@ trajectory part runs unchanged with ``from mops_amd import pyMOPS``:
     MOPS_GetCategoryTime / MOPS_GetTotalTime   (:457-475)
 
 Every trajectory goes through the HIP engine (``engine.run_trajectories`` on
-the C ABI); there is no CPU path.  Out of scope: the netCDF/YAML
-readers (``init_from_reader`` / ``init_from_yaml``) and image remapping
-(``MOPS_RunRemapping`` / ``MOPS_RunReGrid``) raise ``NotImplementedError``.
+the C ABI); there is no CPU path.  ``MPASOReader`` / ``init_from_reader``
+load MPAS netCDF classic files (mops_amd/mpas.py).  Out of scope:
+image remapping (``MOPS_RunRemapping`` / ``MOPS_RunReGrid``) raises
+``NotImplementedError``.
 """
 from __future__ import annotations
 
@@ -31,6 +32,7 @@ import numpy as np
 
 from . import engine as _E
 from . import _lib as _L
+from .mpas import MPASOReader  # noqa: F401  (bindings.cpp:88-91: readGridData / readSolData)
 
 
 class CalcDirection(enum.IntEnum):
@@ -93,10 +95,21 @@ class MPASOGrid:
         self.ints = {}
 
     def init_from_reader(self, reader):
-        raise NotImplementedError("MPAS netCDF reader is out of scope for the trajectory engine (DESIGN.md)")
+        """MPASOGrid::initGrid(MPASOReader*) (MPASOGrid.cpp:190-230)."""
+        G = GridAttributeType
+        self.mCellsSize, self.mEdgesSize = reader.mCellsSize, reader.mEdgesSize
+        self.mMaxEdgesSize, self.mVertexSize = reader.mMaxEdgesSize, reader.mVertexSize
+        self.mVertLevels, self.mVertLevelsP1 = reader.mVertLevels, reader.mVertLevelsP1
+        self.vec3 = {G.kCellCoord: reader.cellCoord_vec, G.kVertexCoord: reader.vertexCoord_vec,
+                     G.kEdgeCoord: reader.edgeCoord_vec}
+        self.ints = {G.kVerticesOnCell: reader.verticesOnCell_vec, G.kVerticesOnEdge: reader.verticesOnEdge_vec,
+                     G.kCellsOnVertex: reader.cellsOnVertex_vec, G.kCellsOnCell: reader.cellsOnCell_vec,
+                     G.kNumberVertexOnCell: reader.numberVertexOnCell_vec, G.kCellsOnEdge: reader.cellsOnEdge_vec,
+                     G.kEdgesOnCell: reader.edgesOnCell_vec}
 
-    def init_from_yaml(self, *a, **k):
-        raise NotImplementedError("ftk YAML stream loading is out of scope for the trajectory engine (DESIGN.md)")
+    def init_from_yaml(self, yaml_path):
+        """MPASOGrid::initGrid_DemoLoading (MPASOGrid.cpp:14-27)."""
+        self.init_from_reader(MPASOReader.readGridData(yaml_path))
 
     def setGridAttribute(self, type, val: int):
         name = _GRID_SCALARS.get(GridAttributeType(type))
@@ -136,28 +149,51 @@ class MPASOSolution:
     def __init__(self):
         self.mCellsSize = self.mEdgesSize = self.mMaxEdgesSize = self.mVertexSize = 0
         self.mVertLevels = self.mVertLevelsP1 = 0
-        self.mTimesteps = self.mID = 0
+        self.mTimesteps = 0
+        self.mID = ("", 0)                      # SolutionID {timeStamp, timestep} (MPASOSolution.h:12-16)
         self.mTimeStamp = ""
         self.doubles = {}
         self.cellCenterVelocity = None
         self.cellVertVelocity_vec = None        # [C*(L+1)] vertVelocityTop; None => zero
+        self.cellSurfaceHeight = None
         self.mDoubleAttributes = {}
 
     def init_from_reader(self, reader):
-        raise NotImplementedError("MPAS netCDF reader is out of scope for the trajectory engine (DESIGN.md)")
+        """MPASOSolution::initSolution(MPASOReader*): raw per-cell arrays, sizes and time stamp."""
+        A = AttributeType
+        self.mVertLevels, self.mVertLevelsP1 = reader.mVertLevels, reader.mVertLevelsP1
+        self.mTimesteps = reader.mTimesteps
+        self.mTimeStamp = reader.mTimeStamp
+        self.mID = (self.mTimeStamp, self.mTimesteps)   # MPASOSolution.cpp:298-299
+        self.doubles = {k: v for k, v in ((A.kLayerThickness, reader.cellLayerThickness_vec),
+                                          (A.kBottomDepth, reader.cellBottomDepth_vec),
+                                          (A.kZonalVelocity, reader.cellZonalVelocity_vec),
+                                          (A.kMeridionalVelocity, reader.cellMeridionalVelocity_vec),
+                                          (A.kZTop, reader.cellZTop_vec),
+                                          (A.kNormalVelocity, reader.cellNormalVelocity_vec)) if v.size}
+        self.cellSurfaceHeight = reader.cellSurfaceHeight_vec if reader.cellSurfaceHeight_vec.size else None
+        self.cellVertVelocity_vec = reader.cellVertVelocity_vec if reader.cellVertVelocity_vec.size else None
+        for k, v in getattr(reader, "attributes", {}).items():
+            self.mDoubleAttributes[k] = v
 
-    def init_from_yaml(self, *a, **k):
-        raise NotImplementedError("ftk YAML stream loading is out of scope for the trajectory engine (DESIGN.md)")
+    def init_from_yaml(self, yaml_path, data_name="", timestep=0):
+        self.init_from_reader(MPASOReader.readSolData(yaml_path, data_name, timestep))
 
-    def add_attribute(self, name: str, arr):
-        self.mDoubleAttributes[name] = np.ascontiguousarray(arr, dtype=np.float64).reshape(-1)
+    def add_attribute(self, name: str, arr=None):
+        """Explicit array, or (pyMOPSAPI: ``add_attribute("temperature", AttributeFormat.kFloat)``) a name the
+        reader already loaded; attributes are unobservable in trajectory outputs (Q9)."""
+        if arr is not None and not isinstance(arr, (int, enum.Enum)):
+            self.mDoubleAttributes[name] = np.ascontiguousarray(arr, dtype=np.float64).reshape(-1)
 
     def setTimestep(self, t: int):
-        self.mTimesteps = int(t)
-        self.mID = int(t)
+        self.mTimesteps = int(t)                # like the reference, mID is untouched
 
     def getID(self) -> int:
-        return self.mID
+        """32-bit FNV-1a of "<timeStamp>_<timestep>" as a signed int (MPASOSolution.h:74-86)."""
+        h = 2166136261
+        for c in f"{self.mID[0]}_{self.mID[1]}".encode():
+            h = ((h ^ c) * 16777619) & 0xFFFFFFFF
+        return h - (1 << 32) if h >= (1 << 31) else h
 
     def getTimeStamp(self) -> str:
         return self.mTimeStamp
@@ -337,7 +373,7 @@ def MOPS_End():
         for sid, s in sorted(_app.sols.items()):
             snap = types.SimpleNamespace(
                 timestep=s.mTimesteps, layerThickness=s.doubles.get(A.kLayerThickness),
-                bottomDepth=s.doubles.get(A.kBottomDepth), surfaceHeight=None,
+                bottomDepth=s.doubles.get(A.kBottomDepth), surfaceHeight=s.cellSurfaceHeight,
                 zonalVelocity=s.doubles.get(A.kZonalVelocity),
                 meridionalVelocity=s.doubles.get(A.kMeridionalVelocity), vertVelocityTop=s.cellVertVelocity_vec)
             _app.fields[sid] = _E.DeviceField.from_snapshot(_app.mesh, snap)

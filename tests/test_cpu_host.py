@@ -41,7 +41,7 @@ def test_frequency_for_cells():
 
 # ---------------------------------------------------------------- C ABI
 def _header_functions():
-    src = "".join(open(os.path.join(ROOT, "include", h)).read() for h in ("mops_traj.h", "mops_io.h"))
+    src = "".join(open(os.path.join(ROOT, "include", h)).read() for h in ("mops_traj.h", "mops_io.h", "mops_netcdf.h"))
     src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
     return sorted(set(re.findall(r"\b(mops_[a-z_0-9]+)\s*\(", src)))
 
