@@ -150,8 +150,20 @@ __device__ __forceinline__ double dmax(double a, double b) { return (a < b) ? b 
 __device__ __forceinline__ double dmin(double a, double b) { return (b < a) ? b : a; }  // std::min
 __device__ __forceinline__ double dclamp(double v, double lo, double hi) { return (v < lo) ? lo : (hi < v) ? hi : v; }
 
-#ifndef MOPS_CELL_REGCACHE
-#define MOPS_CELL_REGCACHE 1  // 1: polygon xyz + B_i live in registers across steps; 0: re-read per evaluation
+// Per-mode polygon cache (swept on MI355X): 1 = vertex xyz + B_i
+// live in registers while the particle stays in its cell; 0 = re-read per
+// evaluation (L1-resident), which frees ~56 VGPRs for the heavier modes.
+#ifndef MOPS_RC_SE
+#define MOPS_RC_SE 1
+#endif
+#ifndef MOPS_RC_SR
+#define MOPS_RC_SR 1
+#endif
+#ifndef MOPS_RC_PE
+#define MOPS_RC_PE 0
+#endif
+#ifndef MOPS_RC_PR
+#define MOPS_RC_PR 0
 #endif
 
 // Per-cell stencil cached in registers while the particle stays in the cell.
@@ -163,16 +175,15 @@ struct Cell {
     double cx, cy, cz;  // cell centre
     double rs2;         // squared "stay" radius (see traj_kernel's walk)
     int vid[MAXV];
-#if MOPS_CELL_REGCACHE
+    int V;              // vertex count (index of the all-zero level-pair record is V*(L-1))
+    bool rc;            // compile-time constant per kernel (load_cell<MAXV, RC>): which members below are live
     double x[MAXV], y[MAXV], z[MAXV];
     double B[MAXV];  // Wachspress B_i = area(poly[i-1], poly[i], poly[i+1]) (depends on the polygon only)
-#else
-    const double4* __restrict__ vxyz;   // polygon re-read per evaluation (L1-resident)
-    const double* __restrict__ cellB;   // per-cell B_i [C][MAXV], computed by cell_b_kernel
-#endif
+    const double4* __restrict__ vxyz;   // rc == false: polygon re-read per evaluation (L1-resident)
+    const double* __restrict__ cellB;   // rc == false: per-cell B_i [C][MAXV] (cell_b_kernel)
 };
 
-template <int MAXV>
+template <int MAXV, bool RC>
 __device__ __forceinline__ void load_cell(Cell<MAXV>& c, int cell, const int* __restrict__ cellrec,
                                           const double4* __restrict__ vxyz, const uint8_t* __restrict__ mono0,
                                           const uint8_t* __restrict__ mono1, const double4* __restrict__ cxyz,
@@ -194,43 +205,42 @@ __device__ __forceinline__ void load_cell(Cell<MAXV>& c, int cell, const int* __
     c.id = cell;
     c.nv = buf[0];
     const int nv = c.nv;
-#if MOPS_CELL_REGCACHE
-#pragma unroll
-    for (int k = 0; k < MAXV; ++k) {
-        c.vid[k] = buf[1 + k];
-        if (k < nv) {
-            const double4 p = vxyz[c.vid[k]];
-            c.x[k] = p.x; c.y[k] = p.y; c.z[k] = p.z;
-        } else {
-            c.x[k] = 0.0; c.y[k] = 0.0; c.z[k] = 0.0;
-        }
-    }
-    double lx = 0, ly = 0, lz = 0;  // poly[nv-1]
-#pragma unroll
-    for (int k = 0; k < MAXV; ++k)
-        if (k == nv - 1) { lx = c.x[k]; ly = c.y[k]; lz = c.z[k]; }
-#pragma unroll
-    for (int i = 0; i < MAXV; ++i) {
-        if (i < nv) {
-            const double qx = (i == 0) ? lx : c.x[(i + MAXV - 1) % MAXV];
-            const double qy = (i == 0) ? ly : c.y[(i + MAXV - 1) % MAXV];
-            const double qz = (i == 0) ? lz : c.z[(i + MAXV - 1) % MAXV];
-            const bool wrap = (i + 1 >= nv);
-            const double nx = wrap ? c.x[0] : c.x[(i + 1) % MAXV];
-            const double ny = wrap ? c.y[0] : c.y[(i + 1) % MAXV];
-            const double nz = wrap ? c.z[0] : c.z[(i + 1) % MAXV];
-            c.B[i] = tri_area(qx, qy, qz, c.x[i], c.y[i], c.z[i], nx, ny, nz);
-        } else {
-            c.B[i] = 0.0;
-        }
-    }
-    (void)cellB;
-#else
+    c.rc = RC;
 #pragma unroll
     for (int k = 0; k < MAXV; ++k) c.vid[k] = buf[1 + k];
-    c.vxyz = vxyz;
-    c.cellB = cellB;
-#endif
+    if constexpr (RC) {
+#pragma unroll
+        for (int k = 0; k < MAXV; ++k) {
+            if (k < nv) {
+                const double4 p = vxyz[c.vid[k]];
+                c.x[k] = p.x; c.y[k] = p.y; c.z[k] = p.z;
+            } else {
+                c.x[k] = 0.0; c.y[k] = 0.0; c.z[k] = 0.0;
+            }
+        }
+        double lx = 0, ly = 0, lz = 0;  // poly[nv-1]
+#pragma unroll
+        for (int k = 0; k < MAXV; ++k)
+            if (k == nv - 1) { lx = c.x[k]; ly = c.y[k]; lz = c.z[k]; }
+#pragma unroll
+        for (int i = 0; i < MAXV; ++i) {
+            if (i < nv) {
+                const double qx = (i == 0) ? lx : c.x[(i + MAXV - 1) % MAXV];
+                const double qy = (i == 0) ? ly : c.y[(i + MAXV - 1) % MAXV];
+                const double qz = (i == 0) ? lz : c.z[(i + MAXV - 1) % MAXV];
+                const bool wrap = (i + 1 >= nv);
+                const double nx = wrap ? c.x[0] : c.x[(i + 1) % MAXV];
+                const double ny = wrap ? c.y[0] : c.y[(i + 1) % MAXV];
+                const double nz = wrap ? c.z[0] : c.z[(i + 1) % MAXV];
+                c.B[i] = tri_area(qx, qy, qz, c.x[i], c.y[i], c.z[i], nx, ny, nz);
+            } else {
+                c.B[i] = 0.0;
+            }
+        }
+    } else {
+        c.vxyz = vxyz;
+        c.cellB = cellB;
+    }
 }
 
 // guards + TBBKernel::IsInMesh + Interpolator::CalcPolygonWachspress
@@ -242,13 +252,12 @@ __device__ __forceinline__ bool weights(const Cell<MAXV>& c, int L, int V, doubl
     const int nv = c.nv;
     if (nv <= 0 || nv > kMaxVertex) return false;
     if (!isfinite(px) || !isfinite(py) || !isfinite(pz)) return false;
-#if MOPS_CELL_REGCACHE
-    const double* X = c.x; const double* Y = c.y; const double* Z = c.z; const double* BB = c.B;
-#else
     double X[MAXV], Y[MAXV], Z[MAXV], BB[MAXV];
 #pragma unroll
     for (int k = 0; k < MAXV; ++k) {
-        if (k < nv) {
+        if (c.rc) {
+            X[k] = c.x[k]; Y[k] = c.y[k]; Z[k] = c.z[k]; BB[k] = c.B[k];
+        } else if (k < nv) {
             const double4 q = c.vxyz[c.vid[k]];
             X[k] = q.x; Y[k] = q.y; Z[k] = q.z;
             BB[k] = c.cellB[(int64_t)c.id * MAXV + k];
@@ -256,7 +265,6 @@ __device__ __forceinline__ bool weights(const Cell<MAXV>& c, int L, int V, doubl
             X[k] = 0.0; Y[k] = 0.0; Z[k] = 0.0; BB[k] = 0.0;
         }
     }
-#endif
 #pragma unroll
     for (int k = 0; k < MAXV; ++k) {
         if (k < nv) {
@@ -512,21 +520,44 @@ struct Pair {
     double um0, um1, um2, uk0, uk1, uk2;  // horizontal velocity at levels k-1, k
 };
 
-template <int MAXV>
+// Weighted sums of the level-pair records of one layer over the stencil.
+// Vertices are taken GR at a time under one `v < nv` branch, so GR records are
+// in flight per memory round trip (PairGroup: 2 for RK4, whose four
+// evaluations per step leave latency exposed; 1 for Euler, where the extra
+// VGPRs cost a wave per SIMD -- measured).  A slot v >= nv inside a group reads the all-zero
+// record at index V*(L-1) with weight 0 and adds +0.0: a sum that starts at
+// +0.0 and only adds products is never -0.0 (x + -x = +0 under
+// round-to-nearest) and S + +0.0 == S otherwise (NaN, inf included), so
+// every sum keeps the bits of the reference's nv-term loop.
+template <int MAXV, int GR>
 __device__ __forceinline__ void pair_sums(const Cell<MAXV>& c, const double* w, const double* __restrict__ pr, int L,
                                           int k, Pair& S) {
     S.z0 = S.zm = S.zk = S.wm = S.wk = 0.0;
     S.um0 = S.um1 = S.um2 = S.uk0 = S.uk1 = S.uk2 = 0.0;
+    const int64_t zrec = (int64_t)c.V * (L - 1);
 #pragma unroll
-    for (int v = 0; v < MAXV; ++v) {
-        if (v < c.nv) {
-            const double2* r = reinterpret_cast<const double2*>(pr + ((int64_t)c.vid[v] * (L - 1) + (k - 1)) * 12);
-            const double2 a0 = r[0], a1 = r[1], a2 = r[2], a3 = r[3], a4 = r[4], a5 = r[5];
-            const double wv = w[v];
-            S.z0 += wv * a0.x; S.zm += wv * a0.y; S.zk += wv * a1.x;
-            S.wm += wv * a1.y; S.wk += wv * a2.x;
-            S.um0 += wv * a2.y; S.um1 += wv * a3.x; S.um2 += wv * a3.y;
-            S.uk0 += wv * a4.x; S.uk1 += wv * a4.y; S.uk2 += wv * a5.x;
+    for (int v0 = 0; v0 < MAXV; v0 += GR) {
+        if (v0 < c.nv) {
+            double2 a[GR][6];
+#pragma unroll
+            for (int j = 0; j < GR; ++j) {
+                const int v = v0 + j;
+                if (v >= MAXV) break;
+                const int64_t ri = (v < c.nv) ? (int64_t)c.vid[v] * (L - 1) + (k - 1) : zrec;
+                const double2* r = reinterpret_cast<const double2*>(pr + ri * 12);
+#pragma unroll
+                for (int q = 0; q < 6; ++q) a[j][q] = r[q];
+            }
+#pragma unroll
+            for (int j = 0; j < GR; ++j) {
+                const int v = v0 + j;
+                if (v >= MAXV) break;
+                const double wv = w[v];
+                S.z0 += wv * a[j][0].x; S.zm += wv * a[j][0].y; S.zk += wv * a[j][1].x;
+                S.wm += wv * a[j][1].y; S.wk += wv * a[j][2].x;
+                S.um0 += wv * a[j][2].y; S.um1 += wv * a[j][3].x; S.um2 += wv * a[j][3].y;
+                S.uk0 += wv * a[j][4].x; S.uk1 += wv * a[j][4].y; S.uk2 += wv * a[j][5].x;
+            }
         }
     }
 }
@@ -537,13 +568,13 @@ __device__ __forceinline__ void pair_sums(const Cell<MAXV>& c, const double* w, 
 // bracket_scan), i.e. a = b = h, which both the binary search (streamline)
 // and the linear scan (pathline) resolve to h.  Otherwise the exact general
 // bracket runs and the record of the final layer is read.
-template <int MAXV, bool PATH>
+template <int MAXV, bool PATH, int GR>
 __device__ __forceinline__ int layer_eval(const Cell<MAXV>& c, const double* w, bool mono_ok, const Field& f, int L,
                                           double d, int& hint, Pair& S) {
     const double eps = 1e-8;
     const int h = hint;
     if (mono_ok && h >= 1 && h <= L - 1) {
-        pair_sums<MAXV>(c, w, f.pr, L, h, S);
+        pair_sums<MAXV, GR>(c, w, f.pr, L, h, S);
         bool ok;
         if (d > S.z0 + eps) {
             ok = (h == 1);
@@ -564,21 +595,21 @@ __device__ __forceinline__ int layer_eval(const Cell<MAXV>& c, const double* w, 
         hint = layer;
     }
     if (layer < 0) return -1;
-    pair_sums<MAXV>(c, w, f.pr, L, layer, S);
+    pair_sums<MAXV, GR>(c, w, f.pr, L, layer, S);
     S.zk = zdn;  // the bracket's (possibly fixed-up) column values
     S.zm = zup;
     return layer;
 }
 
 // streamline calc_velocity_at (MPASOVisualizerKernels.cpp:740-872)
-template <int MAXV>
+template <int MAXV, int GR>
 __device__ __forceinline__ bool eval_stream(const Cell<MAXV>& c, int L, int V, const Field& f, double px, double py,
                                             double pz, double d, int& hint, double& hx, double& hy, double& hz,
                                             double& wv) {
     double w[MAXV];
     if (!weights<MAXV>(c, L, V, px, py, pz, w)) return false;
     Pair S;
-    const int layer = layer_eval<MAXV, false>(c, w, c.mono0 && weights_finite<MAXV>(c, w), f, L, d, hint, S);
+    const int layer = layer_eval<MAXV, false, GR>(c, w, c.mono0 && weights_finite<MAXV>(c, w), f, L, d, hint, S);
     if (layer < 0) return false;
     const double zdn = S.zk, zup = S.zm;
     double x = d;
@@ -599,7 +630,7 @@ __device__ __forceinline__ bool eval_stream(const Cell<MAXV>& c, int L, int V, c
 // pathline calc_velocity_at (MPASOVisualizerKernels.cpp:1124-1327).  The
 // attribute channel is not evaluated: FinalizeTrajectoryLinesWithAttrs never
 // reads it (TrajectoryCommon.h:176-185, quirk Q9), so it is unobservable.
-template <int MAXV>
+template <int MAXV, int GR>
 __device__ __forceinline__ bool eval_path(const Cell<MAXV>& c, int L, int V, const Field& ff, const Field& fb,
                                           double px, double py, double pz, double d, double alpha, int& hint0,
                                           int& hint1, double& hx, double& hy, double& hz, double& wv) {
@@ -607,8 +638,8 @@ __device__ __forceinline__ bool eval_path(const Cell<MAXV>& c, int L, int V, con
     if (!weights<MAXV>(c, L, V, px, py, pz, w)) return false;
     const bool wfin = weights_finite<MAXV>(c, w);
     Pair F, B;
-    const int lf = layer_eval<MAXV, true>(c, w, c.mono0 && wfin, ff, L, d, hint0, F);
-    const int lb = layer_eval<MAXV, true>(c, w, c.mono1 && wfin, fb, L, d, hint1, B);
+    const int lf = layer_eval<MAXV, true, GR>(c, w, c.mono0 && wfin, ff, L, d, hint0, F);
+    const int lb = layer_eval<MAXV, true, GR>(c, w, c.mono1 && wfin, fb, L, d, hint1, B);
     if (lf < 0 || lb < 0) return false;
     const double xf = dmax(F.zk, dmin(d, F.zm));
     const double denf = F.zm - F.zk;
@@ -674,6 +705,14 @@ struct TrajArgs {
 #ifndef MOPS_W_PR
 #define MOPS_W_PR 2  // pathline RK4
 #endif
+template <bool EULER>
+struct PairGroup {
+    static constexpr int value = EULER ? 1 : 2;
+};
+template <bool PATH, bool EULER>
+struct RCache {
+    static constexpr bool value = PATH ? (EULER ? MOPS_RC_PE : MOPS_RC_PR) : (EULER ? MOPS_RC_SE : MOPS_RC_SR);
+};
 template <bool PATH, bool EULER>
 struct TrajWaves {
     static constexpr int value = PATH ? (EULER ? MOPS_W_PE : MOPS_W_PR) : (EULER ? MOPS_W_SE : MOPS_W_SR);
@@ -697,18 +736,19 @@ __global__ void __launch_bounds__(kTrajBlock, (TrajWaves<PATH, EULER>::value)) t
     dev::Cell<MAXV> c;
     c.id = -1;
     c.nv = 0;
+    c.V = a.V;
     const int C = a.C;
     for (int64_t step = a.step_begin; step < a.step_end; ++step) {
         if (step == 0) {  // first_loop (:892-901)
             if (cell < 0 || cell >= C) { died = 0; break; }
-            dev::load_cell<MAXV>(c, cell, a.cellrec, a.vxyz, a.mono0, a.mono1, a.cxyz, a.cellB);
+            dev::load_cell<MAXV, RCache<PATH, EULER>::value>(c, cell, a.cellrec, a.vxyz, a.mono0, a.mono1, a.cxyz, a.cellB);
             double* r0 = a.rec;
             r0[0 * a.rec_stride + pid] = x;
             r0[1 * a.rec_stride + pid] = y;
             r0[2 * a.rec_stride + pid] = z;
         } else {  // one-hop nearest-centre walk (:902-922)
             if (cell < 0 || cell >= C) { died = (int)step; break; }
-            if (c.id != cell) dev::load_cell<MAXV>(c, cell, a.cellrec, a.vxyz, a.mono0, a.mono1, a.cxyz, a.cellB);
+            if (c.id != cell) dev::load_cell<MAXV, RCache<PATH, EULER>::value>(c, cell, a.cellrec, a.vxyz, a.mono0, a.mono1, a.cxyz, a.cellB);
             // Exact shortcut: if |p - c| < rs (half the distance to the nearest
             // neighbour centre, minus 1 m), every neighbour is strictly farther
             // than the current centre by far more than rounding, so the
@@ -727,7 +767,7 @@ __global__ void __launch_bounds__(kTrajBlock, (TrajWaves<PATH, EULER>::value)) t
                     }
                 }
                 cell = nc;
-                if (c.id != cell) dev::load_cell<MAXV>(c, cell, a.cellrec, a.vxyz, a.mono0, a.mono1, a.cxyz, a.cellB);
+                if (c.id != cell) dev::load_cell<MAXV, RCache<PATH, EULER>::value>(c, cell, a.cellrec, a.vxyz, a.mono0, a.mono1, a.cxyz, a.cellB);
             }
         }
         const double d = -1.0 * (double)dep;
@@ -736,8 +776,8 @@ __global__ void __launch_bounds__(kTrajBlock, (TrajWaves<PATH, EULER>::value)) t
         double nx, ny, nz;
         const double alpha = PATH ? (double)step / (double)a.n_steps : 0.0;
         if (EULER) {
-            bool ok = PATH ? dev::eval_path<MAXV>(c, a.L, a.V, a.f0, a.f1, x, y, z, d, alpha, hint0, hint1, hx, hy, hz, wv)
-                           : dev::eval_stream<MAXV>(c, a.L, a.V, a.f0, x, y, z, d, hint0, hx, hy, hz, wv);
+            bool ok = PATH ? dev::eval_path<MAXV, PairGroup<EULER>::value>(c, a.L, a.V, a.f0, a.f1, x, y, z, d, alpha, hint0, hint1, hx, hy, hz, wv)
+                           : dev::eval_stream<MAXV, PairGroup<EULER>::value>(c, a.L, a.V, a.f0, x, y, z, d, hint0, hx, hy, hz, wv);
             if (!ok) { died = (int)step; break; }
             const double ax = y * hz - z * hy, ay = z * hx - x * hz, az = x * hy - y * hx;
             const double speed = dev::len3(hx, hy, hz);
@@ -748,22 +788,22 @@ __global__ void __launch_bounds__(kTrajBlock, (TrajWaves<PATH, EULER>::value)) t
             double s1x, s1y, s1z, s1w, s2x, s2y, s2z, s2w, s3x, s3y, s3z, s3w, s4x, s4y, s4z, s4w;
             double qx, qy, qz;
             const double a1 = alpha;
-            bool ok = PATH ? dev::eval_path<MAXV>(c, a.L, a.V, a.f0, a.f1, x, y, z, d, a1, hint0, hint1, s1x, s1y, s1z, s1w)
-                           : dev::eval_stream<MAXV>(c, a.L, a.V, a.f0, x, y, z, d, hint0, s1x, s1y, s1z, s1w);
+            bool ok = PATH ? dev::eval_path<MAXV, PairGroup<EULER>::value>(c, a.L, a.V, a.f0, a.f1, x, y, z, d, a1, hint0, hint1, s1x, s1y, s1z, s1w)
+                           : dev::eval_stream<MAXV, PairGroup<EULER>::value>(c, a.L, a.V, a.f0, x, y, z, d, hint0, s1x, s1y, s1z, s1w);
             if (!ok) { died = (int)step; break; }
             dev::advect(x, y, z, s1x, s1y, s1z, dt * 0.5, qx, qy, qz);
             const double a2 = PATH ? dev::dclamp(a1 + 0.5 * a.dalpha, 0.0, 1.0) : 0.0;
-            ok = PATH ? dev::eval_path<MAXV>(c, a.L, a.V, a.f0, a.f1, qx, qy, qz, d, a2, hint0, hint1, s2x, s2y, s2z, s2w)
-                      : dev::eval_stream<MAXV>(c, a.L, a.V, a.f0, qx, qy, qz, d, hint0, s2x, s2y, s2z, s2w);
+            ok = PATH ? dev::eval_path<MAXV, PairGroup<EULER>::value>(c, a.L, a.V, a.f0, a.f1, qx, qy, qz, d, a2, hint0, hint1, s2x, s2y, s2z, s2w)
+                      : dev::eval_stream<MAXV, PairGroup<EULER>::value>(c, a.L, a.V, a.f0, qx, qy, qz, d, hint0, s2x, s2y, s2z, s2w);
             if (!ok) { died = (int)step; break; }
             dev::advect(x, y, z, s2x, s2y, s2z, dt * 0.5, qx, qy, qz);
-            ok = PATH ? dev::eval_path<MAXV>(c, a.L, a.V, a.f0, a.f1, qx, qy, qz, d, a2, hint0, hint1, s3x, s3y, s3z, s3w)
-                      : dev::eval_stream<MAXV>(c, a.L, a.V, a.f0, qx, qy, qz, d, hint0, s3x, s3y, s3z, s3w);
+            ok = PATH ? dev::eval_path<MAXV, PairGroup<EULER>::value>(c, a.L, a.V, a.f0, a.f1, qx, qy, qz, d, a2, hint0, hint1, s3x, s3y, s3z, s3w)
+                      : dev::eval_stream<MAXV, PairGroup<EULER>::value>(c, a.L, a.V, a.f0, qx, qy, qz, d, hint0, s3x, s3y, s3z, s3w);
             if (!ok) { died = (int)step; break; }
             dev::advect(x, y, z, s3x, s3y, s3z, dt, qx, qy, qz);
             const double a4 = PATH ? dev::dclamp(a1 + a.dalpha, 0.0, 1.0) : 0.0;
-            ok = PATH ? dev::eval_path<MAXV>(c, a.L, a.V, a.f0, a.f1, qx, qy, qz, d, a4, hint0, hint1, s4x, s4y, s4z, s4w)
-                      : dev::eval_stream<MAXV>(c, a.L, a.V, a.f0, qx, qy, qz, d, hint0, s4x, s4y, s4z, s4w);
+            ok = PATH ? dev::eval_path<MAXV, PairGroup<EULER>::value>(c, a.L, a.V, a.f0, a.f1, qx, qy, qz, d, a4, hint0, hint1, s4x, s4y, s4z, s4w)
+                      : dev::eval_stream<MAXV, PairGroup<EULER>::value>(c, a.L, a.V, a.f0, qx, qy, qz, d, hint0, s4x, s4y, s4z, s4w);
             if (!ok) { died = (int)step; break; }
             // (s1 + 2 s2 + 2 s3 + s4) / 6 -- cy::Vec3 operator order (:959-960)
             hx = (((s1x + s2x * 2.0) + s3x * 2.0) + s4x) / 6.0;
@@ -1391,7 +1431,9 @@ int64_t mops_mesh_bytes(const mops_mesh* mesh) { return mesh ? mesh->bytes : 0; 
 
 static mops_status compute_mono(const mops_mesh* mesh, mops_field* f, hipStream_t s) {
     const int64_t npr = mesh->V * (int64_t)std::max(mesh->L - 1, 0);
-    MOPS_TRY(dmalloc(&f->d_pr, (size_t)std::max<int64_t>(npr * 12, 1), &f->bytes));
+    // + one all-zero record at index npr: pair_sums reads it for v >= nv
+    MOPS_TRY(dmalloc(&f->d_pr, (size_t)((npr + 1) * 12), &f->bytes));
+    HIP_TRY(hipMemsetAsync(f->d_pr + npr * 12, 0, 12 * sizeof(double), s));
     if (npr > 0)
         pair_record_kernel<<<grid_for(npr), kBlock, 0, s>>>(mesh->V, mesh->L, f->d_zt, f->d_vel, f->d_w, f->d_pr);
     MOPS_TRY(dmalloc(&f->d_mono, (size_t)mesh->C, &f->bytes));
