@@ -51,9 +51,22 @@ def parse():
                    help="BASELINE.json config: 2 = 1e6-particle 1-day streamline (default); 3 = 1e7-particle "
                         "7-day chained pathline at layer 10, dt 60 s")
     p.add_argument("--pairs", type=int, default=7, help="config 3: snapshot pairs (days)")
+    p.add_argument("--backend", choices=["nccl", "gloo"], default="nccl",
+                   help="collective backend for N > 1 (nccl = RCCL over xGMI; gloo only to rehearse the multi-rank "
+                        "path on one GPU with MOPS_BENCH_ONE_DEVICE=1)")
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--cpu-seconds", type=float, default=12.0, help="target CPU-baseline sample length")
     return p.parse_args()
+
+
+def all_gather_flat(dist, out, inp, backend):
+    """One all-gather of a rank's slab; gloo (rehearsal only) stages through host memory."""
+    if backend == "nccl":
+        dist.all_gather_into_tensor(out, inp)
+    else:
+        o = out.cpu()
+        dist.all_gather_into_tensor(o, inp.cpu())
+        out.copy_(o)
 
 
 def make_seeds(n: int, rank: int) -> np.ndarray:
@@ -109,10 +122,15 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    if os.environ.get("MOPS_BENCH_ONE_DEVICE") == "1":  # rehearsal: every rank on device 0
+        local_rank = 0
     torch.cuda.set_device(local_rank)
     dev = torch.device("cuda", local_rank)
     if world > 1:
-        dist.init_process_group("nccl", device_id=dev)
+        if args.backend == "nccl":
+            dist.init_process_group("nccl", device_id=dev)
+        else:
+            dist.init_process_group("gloo")
 
     from mops_amd import synth
     from mops_amd.engine import DeviceField, DeviceMesh, ParticleSet, TrajectoryConfig
@@ -166,7 +184,7 @@ def main():
                         done.record(compute)
                         comm.wait_event(done)
                         with torch.cuda.stream(comm):
-                            dist.all_gather_into_tensor(gathered[k].view(-1), ps.records[k].view(-1))
+                            all_gather_flat(dist, gathered[k].view(-1), ps.records[k].view(-1), args.backend)
         compute.synchronize()
         comm.synchronize()
 
@@ -190,7 +208,8 @@ def main():
     dead = int((death >= 0).sum().item())
     kms = [a.elapsed_time(b) for (a, b) in kernel_ms]
     avg_kernel_s = (sum(kms) / len(kms)) / 1e3 if kms else float("nan")
-    stats = torch.tensor([elapsed, float(attempted), float(n), float(dead)], dtype=torch.float64, device=dev)
+    stats = torch.tensor([elapsed, float(attempted), float(n), float(dead)], dtype=torch.float64,
+                         device=dev if args.backend == "nccl" else "cpu")
     if world > 1:
         mx = stats.clone(); dist.all_reduce(mx, op=dist.ReduceOp.MAX)
         sm = stats.clone(); dist.all_reduce(sm, op=dist.ReduceOp.SUM)
@@ -290,7 +309,7 @@ def main_chain(args, mesh, dev, world, rank):
             comm.wait_event(done)
             last.record_stream(comm)
             with torch.cuda.stream(comm):
-                dist.all_gather_into_tensor(gathered.view(-1), last.view(-1))
+                all_gather_flat(dist, gathered.view(-1), last.view(-1), args.backend)
 
     def one_call(timed):
         res = chain.run(seeds, depth=args.depth, method=1 if args.method == "euler" else 0, delta_t=args.dt,
@@ -314,7 +333,8 @@ def main_chain(args, mesh, dev, world, rank):
     elapsed = time.perf_counter() - t0
     kms = [a.elapsed_time(b) for (a, b) in timing]
     avg_kernel_s = (sum(kms) / len(kms)) / 1e3
-    stats = torch.tensor([elapsed, float(attempted), float(n)], dtype=torch.float64, device=dev)
+    stats = torch.tensor([elapsed, float(attempted), float(n)], dtype=torch.float64,
+                         device=dev if args.backend == "nccl" else "cpu")
     if world > 1:
         mx = stats.clone(); dist.all_reduce(mx, op=dist.ReduceOp.MAX)
         sm = stats.clone(); dist.all_reduce(sm, op=dist.ReduceOp.SUM)
