@@ -149,7 +149,7 @@ def main():
     cfg = TrajectoryConfig(deltaT=args.dt, simulationDuration=args.duration, recordT=args.record, depth=args.depth,
                            method=1 if args.method == "euler" else 0)
     ps = ParticleSet(dmesh, seeds, args.depth, cfg, device=dev)
-    seed_cells = ps.cell.cpu().numpy()
+    seed_cells = ps.original(ps.cell).cpu().numpy()
     period = ps.record_period(pathline=pathline)
     n_steps = cfg.n_steps
     bounds = list(range(0, n_steps, period)) + [n_steps]
@@ -250,7 +250,8 @@ def main():
                 "cells": mesh.nCells, "vertices": mesh.nVertices, "levels": mesh.nVertLevels,
                 "particles_per_gpu": n, "particles_total": int(n_all), "integration_steps": n_steps,
                 "records": ps.K, "method": args.method, "parallelism": f"particle-shard x{world}",
-                "record_gather": "rccl all_gather per record instant (side stream)" if world > 1 else "none",
+                "record_gather": (f"{'rccl' if args.backend == 'nccl' else 'gloo'} all_gather per record instant "
+                                  "(side stream)") if world > 1 else "none",
             },
             "nominal_particle_steps_per_call": n_all * n_steps,
             "attempted_particle_steps_per_call": attempted_all,
@@ -366,7 +367,8 @@ def main_chain(args, mesh, dev, world, rank):
                 "particles_per_gpu": n, "particles_total": int(n_all), "integration_steps": n_steps,
                 "records_per_pair": args.duration // args.record, "method": args.method,
                 "parallelism": f"particle-shard x{world}",
-                "record_gather": "rccl all_gather of continuation points per pair" if world > 1 else "none"},
+                "record_gather": (f"{'rccl' if args.backend == 'nccl' else 'gloo'} all_gather of continuation points "
+                                  "per pair") if world > 1 else "none"},
             "nominal_particle_steps_per_call": n_all * n_steps,
             "attempted_particle_steps_per_call": attempted_all / args.steps,
             "roofline": {

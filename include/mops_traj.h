@@ -172,10 +172,14 @@ mops_status mops_traj_advance(const mops_mesh* mesh, const mops_field* front, co
  * (src/Common/TrajectoryCommon.h:57-190) on the device: seeds [n*3] and
  * records -> points/velocity [n*(K+1)*3], temperature/salinity [n*(K+1)]
  * (pathline: velocity x/y, reference quirk Q9; streamline: zeros),
- * last point [n*3].  Any output pointer except points may be NULL. */
+ * last point [n*3].  d_line [n] (or NULL = identity) maps particle slot i of
+ * seeds/records to output line d_line[i] -- for particles kept physically in
+ * locality order (the record stores of mops_traj_advance then coalesce).
+ * Any output pointer except points may be NULL. */
 mops_status mops_traj_finalize(int64_t n, int64_t K, const double* d_seeds, const double* d_records,
-                               int64_t record_stride, int32_t pathline, double* d_points, double* d_velocity,
-                               double* d_temperature, double* d_salinity, double* d_last_point, void* stream);
+                               int64_t record_stride, int32_t pathline, const int32_t* d_line, double* d_points,
+                               double* d_velocity, double* d_temperature, double* d_salinity, double* d_last_point,
+                               void* stream);
 
 /* RemoveNaNTrajectoriesAndReindex alone on n lines of P points each, in
  * place (device pointers; [n*P*3], [n*P*3], [n*P], [n*P], out [n*3]). */

@@ -113,7 +113,7 @@ def load(path: str | None = None):
     lib.mops_traj_num_records.argtypes = [P]; lib.mops_traj_num_records.restype = I64
     lib.mops_traj_num_steps.argtypes = [P]; lib.mops_traj_num_steps.restype = I64
     lib.mops_traj_advance.argtypes = [P, P, P, P, P, I64, I64, P, I64, P]; lib.mops_traj_advance.restype = st
-    lib.mops_traj_finalize.argtypes = [I64, I64, P, P, I64, I32, P, P, P, P, P, P]
+    lib.mops_traj_finalize.argtypes = [I64, I64, P, P, I64, I32, P, P, P, P, P, P, P]
     lib.mops_traj_finalize.restype = st
     lib.mops_remove_nan_lines.argtypes = [I64, I64, P, P, P, P, P, P]; lib.mops_remove_nan_lines.restype = st
     lib.mops_run_trajectories.argtypes = [P, P, P, P, I64, P, P, C.c_float, P, P, P, P, P, P, P, P, P, P]

@@ -126,7 +126,7 @@ class PathlineChain:
         if self.own_fields:
             for f in fields.values():
                 f.close()
-        res = dict(lastPoint=last, death_step=ps.death.clone(), attempted=attempted)
+        res = dict(lastPoint=last, death_step=ps.original(ps.death), attempted=attempted)
         if keep_lines:
             res.update(points=torch.cat(pts_acc, 1), velocity=torch.cat(vel_acc, 1), temperature=torch.cat(tmp_acc, 1),
                        salinity=torch.cat(sal_acc, 1))

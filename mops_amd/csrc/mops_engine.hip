@@ -38,7 +38,7 @@
 #include "mops_io.h"
 #include "mops_traj.h"
 
-#define MOPS_ABI_VERSION 1
+#define MOPS_ABI_VERSION 2
 
 namespace {
 
@@ -904,29 +904,58 @@ __global__ void remove_nan_kernel(int64_t n, int64_t P, double* pts, double* vel
     }
 }
 
-__global__ void assemble_kernel(int64_t n, int64_t K, const double* seeds, const double* rec, int64_t stride,
-                                int pathline, double* pts, double* vel, double* tmp, double* sal) {
-    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= n) return;
+// Records [K][6][stride] (slot-major) -> lines [n][P] (line-major): a
+// transpose, staged through LDS in tiles of 32 slots x 8 records so that both
+// the record reads (32 consecutive slots) and the line writes (8 records x 3
+// doubles contiguous per line) coalesce.  Line of slot i = line ? line[i] : i.
+constexpr int kAsmSlots = 32, kAsmRecs = 8;
+__global__ void __launch_bounds__(256) assemble_kernel(int64_t n, int64_t K, const double* __restrict__ seeds,
+                                                       const double* __restrict__ rec, int64_t stride, int pathline,
+                                                       const int32_t* __restrict__ line, double* __restrict__ pts,
+                                                       double* __restrict__ vel, double* __restrict__ tmp,
+                                                       double* __restrict__ sal) {
+    __shared__ double tile[kAsmRecs][6][kAsmSlots + 1];
+    __shared__ int64_t row[kAsmSlots];
+    const int t = threadIdx.x;
+    const int64_t s0 = (int64_t)blockIdx.x * kAsmSlots;
+    const int ns = (int)((n - s0) < kAsmSlots ? (n - s0) : kAsmSlots);
     const int64_t P = K + 1;
-    double* pp = pts + 3 * i * P;
-    pp[0] = seeds[3 * i]; pp[1] = seeds[3 * i + 1]; pp[2] = seeds[3 * i + 2];
-    for (int64_t k = 0; k < K; ++k) {
-        const double* rk = rec + k * 6 * stride;
-        pp[3 * (k + 1)] = rk[i];
-        pp[3 * (k + 1) + 1] = rk[stride + i];
-        pp[3 * (k + 1) + 2] = rk[2 * stride + i];
-        if (vel) {
-            vel[3 * (i * P + k)] = rk[3 * stride + i];
-            vel[3 * (i * P + k) + 1] = rk[4 * stride + i];
-            vel[3 * (i * P + k) + 2] = rk[5 * stride + i];
-        }
-        if (tmp) tmp[i * P + k] = pathline ? rk[3 * stride + i] : 0.0;
-        if (sal) sal[i * P + k] = pathline ? rk[4 * stride + i] : 0.0;
+    if (t < ns) {
+        const int64_t r = line ? (int64_t)line[s0 + t] : s0 + t;
+        row[t] = r;
+        double* pp = pts + 3 * r * P;  // points[0] = seed
+        pp[0] = seeds[3 * (s0 + t)]; pp[1] = seeds[3 * (s0 + t) + 1]; pp[2] = seeds[3 * (s0 + t) + 2];
+        if (vel) { double* vv = vel + 3 * (r * P + K); vv[0] = 0.0; vv[1] = 0.0; vv[2] = 0.0; }  // appended zero
+        if (tmp) tmp[r * P + K] = 0.0;
+        if (sal) sal[r * P + K] = 0.0;
     }
-    if (vel) { vel[3 * (i * P + K)] = 0.0; vel[3 * (i * P + K) + 1] = 0.0; vel[3 * (i * P + K) + 2] = 0.0; }
-    if (tmp) tmp[i * P + K] = 0.0;
-    if (sal) sal[i * P + K] = 0.0;
+    for (int64_t k0 = 0; k0 < K; k0 += kAsmRecs) {
+        const int nk = (int)((K - k0) < kAsmRecs ? (K - k0) : kAsmRecs);
+        __syncthreads();  // previous chunk consumed (and row[] written)
+        for (int e = t; e < kAsmRecs * 6 * kAsmSlots; e += blockDim.x) {
+            const int i = e % kAsmSlots, c = (e / kAsmSlots) % 6, kk = e / (kAsmSlots * 6);
+            if (i < ns && kk < nk) tile[kk][c][i] = rec[(k0 + kk) * 6 * stride + c * stride + s0 + i];
+        }
+        __syncthreads();
+        for (int e = t; e < kAsmSlots * kAsmRecs * 3; e += blockDim.x) {
+            const int i = e / (kAsmRecs * 3), off = e % (kAsmRecs * 3), kk = off / 3, c = off % 3;
+            if (i < ns && kk < nk) {
+                const int64_t r = row[i];
+                pts[3 * (r * P + k0 + kk + 1) + c] = tile[kk][c][i];
+                if (vel) vel[3 * (r * P + k0 + kk) + c] = tile[kk][3 + c][i];
+            }
+        }
+        if (tmp || sal) {
+            for (int e = t; e < kAsmSlots * kAsmRecs; e += blockDim.x) {
+                const int i = e / kAsmRecs, kk = e % kAsmRecs;
+                if (i < ns && kk < nk) {
+                    const int64_t r = row[i];
+                    if (tmp) tmp[r * P + k0 + kk] = pathline ? tile[kk][3][i] : 0.0;
+                    if (sal) sal[r * P + k0 + kk] = pathline ? tile[kk][4][i] : 0.0;
+                }
+            }
+        }
+    }
 }
 
 // ===========================================================================
@@ -1654,14 +1683,15 @@ mops_status mops_traj_advance(const mops_mesh* mesh, const mops_field* front, co
 }
 
 mops_status mops_traj_finalize(int64_t n, int64_t K, const double* d_seeds, const double* d_records,
-                               int64_t stride, int32_t pathline, double* d_points, double* d_vel, double* d_tmp,
-                               double* d_sal, double* d_last, void* stream) {
+                               int64_t stride, int32_t pathline, const int32_t* d_line, double* d_points,
+                               double* d_vel, double* d_tmp, double* d_sal, double* d_last, void* stream) {
     if (n < 0 || K <= 0 || !d_seeds || !d_records || !d_points || stride < n)
         return fail(MOPS_ERR_INVALID, "mops_traj_finalize: invalid argument");
     if (n == 0) return MOPS_OK;
     hipStream_t s = (hipStream_t)stream;
-    assemble_kernel<<<grid_for(n), kBlock, 0, s>>>(n, K, d_seeds, d_records, stride, pathline, d_points, d_vel, d_tmp,
-                                                   d_sal);
+    assemble_kernel<<<(unsigned)((n + kAsmSlots - 1) / kAsmSlots), 256, 0, s>>>(n, K, d_seeds, d_records, stride,
+                                                                               pathline, d_line, d_points, d_vel,
+                                                                               d_tmp, d_sal);
     remove_nan_kernel<<<grid_for(n), kBlock, 0, s>>>(n, K + 1, d_points, d_vel, d_tmp, d_sal, d_last);
     HIP_TRY(hipGetLastError());
     return MOPS_OK;
@@ -1767,7 +1797,8 @@ mops_status mops_run_trajectories(const mops_mesh* mesh, const mops_field* front
         if ((st = mops_order_particles(mesh, n, cells, order, stream)) != MOPS_OK) break;
         mops_particles prt{n, x, y, z, dep, cells, death, order};
         if ((st = mops_traj_advance(mesh, front, back, cfg, &prt, 0, n_steps, rec, n, stream)) != MOPS_OK) break;
-        if ((st = mops_traj_finalize(n, K, seeds, rec, n, back ? 1 : 0, pts, vel, tmp, sal, last, stream)) != MOPS_OK)
+        if ((st = mops_traj_finalize(n, K, seeds, rec, n, back ? 1 : 0, nullptr, pts, vel, tmp, sal, last, stream)) !=
+            MOPS_OK)
             break;
         e = hipMemcpyAsync(h_points, pts, (size_t)(n * P * 3) * sizeof(double), hipMemcpyDeviceToHost, s);
         if (e == hipSuccess && h_vel) e = hipMemcpyAsync(h_vel, vel, (size_t)(n * P * 3) * sizeof(double), hipMemcpyDeviceToHost, s);

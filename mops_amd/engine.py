@@ -9,12 +9,17 @@ every array per call, src/GPU/HIP/Kernel/MPASOVisualizerKernels.cu:1369-1431).
 """
 from __future__ import annotations
 
+import contextlib
 import ctypes as C
 import dataclasses
 
 import numpy as np
 
 from . import _lib as L
+
+
+def _nullcontext():
+    return contextlib.nullcontext()
 
 
 def _ptr(a: np.ndarray | None):
@@ -218,14 +223,40 @@ class ParticleSet:
         self.K = cfg.n_records
         self.records = torch.zeros((max(self.K, 1), 6, self.n), dtype=torch.float64, device=dev)
         self.order = torch.empty((self.n,), dtype=torch.int32, device=dev)
+        # slot -> particle index: with use_order the state is kept PHYSICALLY in
+        # locality order (state loads/stores and record stores coalesce);
+        # finalize() writes line ids[slot], so outputs keep the seed order
+        self.ids = torch.arange(self.n, dtype=torch.int32, device=dev)
+        self._written = False
         self._c = cfg.ctype()
         self.reorder(stream=torch.cuda.current_stream(dev).cuda_stream)
 
     def reorder(self, stream=None):
-        """Locality order of the particles by their current cell (mops_order_particles)."""
+        """Locality order of the particles by their current cell (mops_order_particles), applied by permuting
+        the SoA state (and any records already written) so slot s holds particle ids[s]."""
         L.check(L.load().mops_order_particles(self.mesh.handle, self.n, C.c_void_p(self.cell.data_ptr()),
                                               C.c_void_p(self.order.data_ptr()), _stream_handle(stream)),
                 "mops_order_particles")
+        if not self.use_order or self.n == 0:
+            return
+        torch = self.torch
+        if isinstance(stream, int):
+            s = torch.cuda.ExternalStream(stream) if stream else None
+        else:
+            s = stream
+        with torch.cuda.stream(s) if s is not None else _nullcontext():
+            o = self.order.long()
+            for t in (self.x, self.y, self.z, self.depth, self.cell, self.death, self.ids):
+                t.copy_(t[o])
+            self.seeds.copy_(self.seeds[o])
+            if self._written:
+                self.records.copy_(self.records[:, :, o])
+
+    def original(self, t):
+        """A per-slot tensor back in the particles' seed order."""
+        out = self.torch.empty_like(t)
+        out[self.ids.long()] = t
+        return out
 
     def reset(self, seeds_xyz=None, depth=None):
         if seeds_xyz is not None:
@@ -235,6 +266,7 @@ class ParticleSet:
             self.depth.fill_(float(depth))
         self.death.fill_(-1)
         self.records.zero_()
+        self._written = False
 
     def reseed(self, seeds, depth, stream=None):
         """Start a new run from device-resident seeds [n,3] (f64) and depth (scalar
@@ -245,6 +277,7 @@ class ParticleSet:
         if int(s.shape[0]) != self.n:
             raise ValueError("reseed: particle count changed")
         self.seeds.copy_(s)
+        self.ids.copy_(torch.arange(self.n, dtype=torch.int32, device=self.ids.device))
         self.x.copy_(s[:, 0]); self.y.copy_(s[:, 1]); self.z.copy_(s[:, 2])
         if isinstance(depth, torch.Tensor):
             self.depth.copy_(depth.to(torch.float32))
@@ -252,14 +285,14 @@ class ParticleSet:
             self.depth.fill_(float(np.float32(depth)))
         self.death.fill_(-1)
         self.records.zero_()
+        self._written = False
         h = stream if stream is not None else torch.cuda.current_stream(self.seeds.device).cuda_stream
         self.mesh.locate(self.seeds.data_ptr(), self.cell.data_ptr(), self.n, stream=h)
         self.reorder(stream=h)
 
     def particles(self) -> L.Particles:
         return L.Particles(self.n, self.x.data_ptr(), self.y.data_ptr(), self.z.data_ptr(), self.depth.data_ptr(),
-                           self.cell.data_ptr(), self.death.data_ptr(),
-                           self.order.data_ptr() if self.use_order else None)
+                           self.cell.data_ptr(), self.death.data_ptr(), None)  # physically ordered: no indirection
 
     def advance(self, front: DeviceField, back: DeviceField | None, step_begin: int, step_end: int, stream=None):
         p = self.particles()
@@ -267,6 +300,7 @@ class ParticleSet:
                                         C.byref(self._c), C.byref(p), int(step_begin), int(step_end),
                                         C.c_void_p(self.records.data_ptr()), self.n, _stream_handle(stream))
         L.check(st, "mops_traj_advance")
+        self._written = True
 
     def record_period(self, pathline: bool) -> int:
         import math
@@ -285,7 +319,7 @@ class ParticleSet:
         last = torch.empty((self.n, 3), dtype=torch.float64, device=dev)
         st = L.load().mops_traj_finalize(self.n, self.K, C.c_void_p(self.seeds.data_ptr()),
                                          C.c_void_p(self.records.data_ptr()), self.n, 1 if pathline else 0,
-                                         C.c_void_p(pts.data_ptr()), C.c_void_p(vel.data_ptr()),
+                                         C.c_void_p(self.ids.data_ptr()), C.c_void_p(pts.data_ptr()), C.c_void_p(vel.data_ptr()),
                                          C.c_void_p(tmp.data_ptr()), C.c_void_p(sal.data_ptr()),
                                          C.c_void_p(last.data_ptr()), _stream_handle(stream))
         L.check(st, "mops_traj_finalize")

@@ -226,7 +226,19 @@ def test_order_is_permutation_and_result_invariant(gpu, dev_small, small_case):
     b = ParticleSet(dm, seeds, 300.0, cfg, use_order=False)
     order = a.order.cpu().numpy()
     assert np.array_equal(np.sort(order), np.arange(len(seeds)))
+    assert np.array_equal(np.sort(a.ids.cpu().numpy()), np.arange(len(seeds)))   # state physically permuted
     for ps in (a, b):
         ps.advance(f0, f1, 0, cfg.n_steps)
+    la, lb = a.finalize(pathline=True), b.finalize(pathline=True)
     torch.cuda.synchronize()
-    assert torch.equal(a.records, b.records) and torch.equal(a.death, b.death)
+    for k in ("points", "velocity", "temperature", "salinity", "lastPoint"):
+        assert torch.equal(la[k], lb[k]), k
+    assert torch.equal(a.original(a.death), b.death) and torch.equal(a.original(a.x), b.x)
+    # re-ordering mid-run permutes the records already written, results unchanged
+    c = ParticleSet(dm, seeds, 300.0, cfg, use_order=True)
+    c.advance(f0, f1, 0, 17)
+    c.reorder()
+    c.advance(f0, f1, 17, cfg.n_steps)
+    lc = c.finalize(pathline=True)
+    torch.cuda.synchronize()
+    assert torch.equal(lc["points"], lb["points"]) and torch.equal(lc["velocity"], lb["velocity"])
