@@ -709,17 +709,22 @@ template <bool EULER>
 struct PairGroup {
     static constexpr int value = EULER ? 1 : 2;
 };
-template <bool PATH, bool EULER>
+// Wide stencils (maxEdges > 7: MAXV 12 / 20) never cache the polygon in
+// registers and ask for fewer waves -- their per-vertex arrays alone would
+// otherwise spill.
+template <int MAXV, bool PATH, bool EULER>
 struct RCache {
-    static constexpr bool value = PATH ? (EULER ? MOPS_RC_PE : MOPS_RC_PR) : (EULER ? MOPS_RC_SE : MOPS_RC_SR);
+    static constexpr bool value =
+        MAXV <= 7 && (PATH ? (EULER ? MOPS_RC_PE : MOPS_RC_PR) : (EULER ? MOPS_RC_SE : MOPS_RC_SR));
 };
-template <bool PATH, bool EULER>
+template <int MAXV, bool PATH, bool EULER>
 struct TrajWaves {
-    static constexpr int value = PATH ? (EULER ? MOPS_W_PE : MOPS_W_PR) : (EULER ? MOPS_W_SE : MOPS_W_SR);
+    static constexpr int base = PATH ? (EULER ? MOPS_W_PE : MOPS_W_PR) : (EULER ? MOPS_W_SE : MOPS_W_SR);
+    static constexpr int value = MAXV <= 7 ? base : (EULER ? 2 : 1);
 };
 
 template <int MAXV, bool PATH, bool EULER>
-__global__ void __launch_bounds__(kTrajBlock, (TrajWaves<PATH, EULER>::value)) traj_kernel(TrajArgs a) {
+__global__ void __launch_bounds__(kTrajBlock, (TrajWaves<MAXV, PATH, EULER>::value)) traj_kernel(TrajArgs a) {
     // XCD-aware mapping: blocks b, b+8, ... share an XCD (L2); give each XCD a
     // contiguous range of the locality-ordered particles (bijective remap)
     const unsigned nblk = gridDim.x, b = blockIdx.x, xcd = b % 8u, q = nblk / 8u, r = nblk % 8u;
@@ -741,14 +746,14 @@ __global__ void __launch_bounds__(kTrajBlock, (TrajWaves<PATH, EULER>::value)) t
     for (int64_t step = a.step_begin; step < a.step_end; ++step) {
         if (step == 0) {  // first_loop (:892-901)
             if (cell < 0 || cell >= C) { died = 0; break; }
-            dev::load_cell<MAXV, RCache<PATH, EULER>::value>(c, cell, a.cellrec, a.vxyz, a.mono0, a.mono1, a.cxyz, a.cellB);
+            dev::load_cell<MAXV, RCache<MAXV, PATH, EULER>::value>(c, cell, a.cellrec, a.vxyz, a.mono0, a.mono1, a.cxyz, a.cellB);
             double* r0 = a.rec;
             r0[0 * a.rec_stride + pid] = x;
             r0[1 * a.rec_stride + pid] = y;
             r0[2 * a.rec_stride + pid] = z;
         } else {  // one-hop nearest-centre walk (:902-922)
             if (cell < 0 || cell >= C) { died = (int)step; break; }
-            if (c.id != cell) dev::load_cell<MAXV, RCache<PATH, EULER>::value>(c, cell, a.cellrec, a.vxyz, a.mono0, a.mono1, a.cxyz, a.cellB);
+            if (c.id != cell) dev::load_cell<MAXV, RCache<MAXV, PATH, EULER>::value>(c, cell, a.cellrec, a.vxyz, a.mono0, a.mono1, a.cxyz, a.cellB);
             // Exact shortcut: if |p - c| < rs (half the distance to the nearest
             // neighbour centre, minus 1 m), every neighbour is strictly farther
             // than the current centre by far more than rounding, so the
@@ -767,7 +772,7 @@ __global__ void __launch_bounds__(kTrajBlock, (TrajWaves<PATH, EULER>::value)) t
                     }
                 }
                 cell = nc;
-                if (c.id != cell) dev::load_cell<MAXV, RCache<PATH, EULER>::value>(c, cell, a.cellrec, a.vxyz, a.mono0, a.mono1, a.cxyz, a.cellB);
+                if (c.id != cell) dev::load_cell<MAXV, RCache<MAXV, PATH, EULER>::value>(c, cell, a.cellrec, a.vxyz, a.mono0, a.mono1, a.cxyz, a.cellB);
             }
         }
         const double d = -1.0 * (double)dep;

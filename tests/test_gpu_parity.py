@@ -242,3 +242,26 @@ def test_order_is_permutation_and_result_invariant(gpu, dev_small, small_case):
     lc = c.finalize(pathline=True)
     torch.cuda.synchronize()
     assert torch.equal(lc["points"], lb["points"]) and torch.equal(lc["velocity"], lb["velocity"])
+
+
+@pytest.mark.parametrize("max_edges", [10, 16])
+def test_wide_stencil_instantiations(gpu, engine_lib, oracle_lib, max_edges):
+    """maxEdges > 7 selects the MAXV 12 / 20 kernels (no register polygon
+    cache, fewer waves); results must not depend on the padding width."""
+    from mops_amd import synth
+    from mops_amd.engine import DeviceField, DeviceMesh, TrajectoryConfig, run_trajectories
+    mesh = synth.make_mesh(16, n_levels=10, max_edges=max_edges)
+    s0 = synth.make_snapshot(mesh, timestep=0)
+    s1 = synth.make_snapshot(mesh, timestep=1, phase=0.35)
+    dm = DeviceMesh.from_mesh(mesh)
+    f0, f1 = DeviceField.from_snapshot(dm, s0), DeviceField.from_snapshot(dm, s1)
+    r0, r1 = oracle_lib.preprocess(mesh, s0), oracle_lib.preprocess(mesh, s1)
+    seeds = synth.uniform_band_seeds(300, seed=41)
+    for back, rb in ((None, None), (f1, r1)):
+        for method in (1, 0):
+            cfg = TrajectoryConfig(deltaT=300, simulationDuration=43200, recordT=3600, depth=250.0, method=method)
+            got = run_trajectories(dm, f0, back, cfg, seeds)
+            ref = oracle_lib.run(mesh, r0, rb, seeds, depth=250.0, delta_t=300, duration=43200, record_t=3600,
+                                 euler=(method == 1), cells=got["cells"])
+            assert_lines_match(got, ref, f"maxEdges={max_edges} path={back is not None} method={method}")
+            assert np.array_equal(got["points"], ref["points"])
