@@ -111,7 +111,15 @@ struct mops_field {
 // ===========================================================================
 namespace dev {
 
-__device__ __forceinline__ double len3(double x, double y, double z) { return sqrt(x * x + y * y + z * z); }
+__device__ __forceinline__ double sq3(double x, double y, double z) { return x * x + y * y + z * z; }
+__device__ __forceinline__ double len3(double x, double y, double z) { return sqrt(sq3(x, y, z)); }
+
+// The reference's `length(v) < 1e-12` tests (MPASOVisualizerKernels.cpp:841-852)
+// without the square root: correctly rounded sqrt is monotone, and the
+// smallest double s with sqrt(s) >= 1e-12 is exactly the double 1e-24
+// (0x1.357c299a88ea7p-80; tests/test_cpu_host.py::test_norm_threshold), so
+// sqrt(s) < 1e-12  <=>  s < 1e-24 for every s >= 0, NaN and inf included.
+constexpr double kNormTiny2 = 0x1.357c299a88ea7p-80;
 
 // Interpolator::triangle_area (Interpolation.hpp:95-110)
 __device__ __forceinline__ double tri_area(double ax, double ay, double az, double bx, double by, double bz,
@@ -496,6 +504,62 @@ __device__ __forceinline__ int bracket_mono(const Cell<MAXV>& c, const double* w
     return layer;
 }
 
+// One-hop nearest-centre walk (TBBKernel::GetCellNeighborsIdx, TBBKernel.h:74-101,
+// and the relocation loop, MPASOVisualizerKernels.cpp:902-922): candidates are
+// cellsOnCell[c][0..nv-1] then c itself, entries outside [0, C) skipped, and
+// the first candidate with the smallest Euclidean distance wins (strict <).
+// All neighbour ids and centres are fetched in one batch (the reference's loop
+// order would serialise 2 round trips per candidate), and the argmin runs on
+// squared distances: correctly rounded sqrt is monotone, so the smallest
+// distance is sqrt(min s), and a later candidate ties it only if its s is
+// within a few ulps of min s -- only then is its sqrt taken and compared.  A
+// candidate whose distance is inf or NaN never beats the reference's initial
+// DBL_MAX, so only finite s take part.
+template <int MAXV>
+__device__ __forceinline__ int walk(const Cell<MAXV>& c, int cell, double x, double y, double z,
+                                    const int* __restrict__ cellrec, const double4* __restrict__ cxyz, int C) {
+    constexpr int REC = ((1 + 2 * MAXV) + 3) / 4 * 4;
+    constexpr int Q0 = (1 + MAXV) / 4, Q1 = (2 * MAXV) / 4;  // int4 words holding cellsOnCell
+    int buf[(Q1 - Q0 + 1) * 4];
+    const int4* r4 = reinterpret_cast<const int4*>(cellrec + (int64_t)cell * REC);
+#pragma unroll
+    for (int q = Q0; q <= Q1; ++q) {
+        const int4 v = r4[q];
+        buf[4 * (q - Q0)] = v.x; buf[4 * (q - Q0) + 1] = v.y; buf[4 * (q - Q0) + 2] = v.z; buf[4 * (q - Q0) + 3] = v.w;
+    }
+    int id[MAXV];
+    bool ok[MAXV];
+    double s[MAXV];
+#pragma unroll
+    for (int k = 0; k < MAXV; ++k) {
+        id[k] = buf[1 + MAXV + k - 4 * Q0];
+        ok[k] = (k < c.nv) && id[k] >= 0 && id[k] < C;
+        // unconditional (clamped) loads, so all centres are in flight at once
+        const double4 q = cxyz[ok[k] ? id[k] : cell];
+        const double dx = q.x - x, dy = q.y - y, dz = q.z - z;
+        s[k] = dx * dx + dy * dy + dz * dz;  // len3(q - p) before its sqrt
+    }
+    const double ex = c.cx - x, ey = c.cy - y, ez = c.cz - z;  // c itself (cached centre)
+    const double sc = ex * ex + ey * ey + ez * ez;
+    const double inf = __builtin_huge_val();
+    double bs = inf;
+#pragma unroll
+    for (int k = 0; k < MAXV; ++k)
+        if (ok[k] && s[k] < bs) bs = s[k];
+    if (sc < bs) bs = sc;
+    if (!(bs < inf)) return cell;  // no finite distance: nothing beats DBL_MAX
+    // s > thr  =>  sqrt(s) > sqrt(bs) after rounding (relative gap >> 1 ulp);
+    // below 2^-900 the product rounds coarsely, so every s there is compared exactly
+    const double thr = (bs < 0x1p-900) ? 0x1p-900 : bs * (1.0 + 0x1p-40);
+#pragma unroll
+    for (int k = 0; k < MAXV; ++k) {
+        if (ok[k] && s[k] <= thr) {
+            if (s[k] == bs || sqrt(s[k]) == sqrt(bs)) return id[k];
+        }
+    }
+    return cell;  // c attains the minimum and no earlier candidate ties it
+}
+
 template <int MAXV>
 __device__ __forceinline__ bool weights_finite(const Cell<MAXV>& c, const double* w) {
     bool ok = true;
@@ -618,11 +682,11 @@ __device__ __forceinline__ bool eval_stream(const Cell<MAXV>& c, int L, int V, c
     if (fabs(den) < 1e-12) return false;
     const double t = (x - zdn) / den;
     // vel_dn at `layer`, vel_up at `layer - 1`; w at interfaces layer, layer-1
-    if (len3(S.uk0, S.uk1, S.uk2) < 1e-12 || len3(S.um0, S.um1, S.um2) < 1e-12) return false;
+    if (sq3(S.uk0, S.uk1, S.uk2) < kNormTiny2 || sq3(S.um0, S.um1, S.um2) < kNormTiny2) return false;
     hx = S.um0 * t + S.uk0 * (1.0 - t);
     hy = S.um1 * t + S.uk1 * (1.0 - t);
     hz = S.um2 * t + S.uk2 * (1.0 - t);
-    if (len3(hx, hy, hz) < 1e-12) return false;
+    if (sq3(hx, hy, hz) < kNormTiny2) return false;
     wv = t * S.wm + (1.0 - t) * S.wk;
     return true;
 }
@@ -705,9 +769,15 @@ struct TrajArgs {
 #ifndef MOPS_W_PR
 #define MOPS_W_PR 2  // pathline RK4
 #endif
+#ifndef MOPS_GR_E
+#define MOPS_GR_E 1  // level-pair records in flight per round trip, Euler
+#endif
+#ifndef MOPS_GR_R
+#define MOPS_GR_R 2  // RK4
+#endif
 template <bool EULER>
 struct PairGroup {
-    static constexpr int value = EULER ? 1 : 2;
+    static constexpr int value = EULER ? MOPS_GR_E : MOPS_GR_R;
 };
 // Wide stencils (maxEdges > 7: MAXV 12 / 20) never cache the polygon in
 // registers and ask for fewer waves -- their per-vertex arrays alone would
@@ -760,18 +830,7 @@ __global__ void __launch_bounds__(kTrajBlock, (TrajWaves<MAXV, PATH, EULER>::val
             // reference's argmin (current cell listed last, strict <) keeps c.
             const double ex = x - c.cx, ey = y - c.cy, ez = z - c.cz;
             if (!(ex * ex + ey * ey + ez * ez < c.rs2)) {
-                const int* rec = a.cellrec + (int64_t)cell * (((1 + 2 * MAXV) + 3) / 4 * 4);
-                double best = 1.7976931348623157e308;
-                int nc = cell;
-                for (int n = 0; n <= c.nv; ++n) {
-                    const int cid = (n < c.nv) ? rec[1 + MAXV + n] : cell;
-                    if (cid >= 0 && cid < C) {
-                        const double4 q = a.cxyz[cid];
-                        const double l = dev::len3(q.x - x, q.y - y, q.z - z);
-                        if (l < best) { best = l; nc = cid; }
-                    }
-                }
-                cell = nc;
+                cell = dev::walk<MAXV>(c, cell, x, y, z, a.cellrec, a.cxyz, C);
                 if (c.id != cell) dev::load_cell<MAXV, RCache<MAXV, PATH, EULER>::value>(c, cell, a.cellrec, a.vxyz, a.mono0, a.mono1, a.cxyz, a.cellB);
             }
         }

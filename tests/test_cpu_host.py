@@ -34,6 +34,21 @@ def test_mesh_is_valid_mpas_layout(land):
         assert (m.cellsOnVertex == 0).any()                # culled coast
 
 
+def test_norm_threshold():
+    """The engine tests `x*x+y*y+z*z < 0x1.357c299a88ea7p-80` in place of the
+    reference's `length(v) < 1e-12` (kNormTiny2, mops_engine.hip): the constant
+    is the smallest double whose correctly rounded sqrt is >= 1e-12."""
+    import math
+    import struct
+    t = float.fromhex("0x1.357c299a88ea7p-80")
+    below = struct.unpack("<d", struct.pack("<q", struct.unpack("<q", struct.pack("<d", t))[0] - 1))[0]
+    assert math.sqrt(t) >= 1e-12 and math.sqrt(below) < 1e-12
+    assert t == 1e-24
+    rng = np.random.default_rng(0)
+    s = np.concatenate([rng.uniform(0, 4e-24, 20000), [0.0, t, below, np.inf, np.nan]])
+    assert np.array_equal(np.sqrt(s) < 1e-12, s < t)
+
+
 def test_frequency_for_cells():
     from mops_amd import synth
     assert synth.frequency_for_cells(236000) in (153, 154)
