@@ -180,8 +180,8 @@ struct Cell {
     int id;
     int nv;
     bool mono0, mono1;  // fast-path flags of the cell for the front / back field
-    double cx, cy, cz;  // cell centre
-    double rs2;         // squared "stay" radius (see traj_kernel's walk)
+    double cx, cy, cz;  // "stay" anchor: the cell centre, or the position of the last walk that kept the cell
+    double rs2;         // squared stay radius around the anchor (see dev::walk)
     int vid[MAXV];
     int V;              // vertex count (index of the all-zero level-pair record is V*(L-1))
     bool rc;            // compile-time constant per kernel (load_cell<MAXV, RC>): which members below are live
@@ -515,8 +515,19 @@ __device__ __forceinline__ int bracket_mono(const Cell<MAXV>& c, const double* w
 // within a few ulps of min s -- only then is its sqrt taken and compared.  A
 // candidate whose distance is inf or NaN never beats the reference's initial
 // DBL_MAX, so only finite s take part.
+//
+// Stay anchor.  When the walk keeps c, every neighbour is farther than c by
+// the gap g = sqrt(s_2nd) - sqrt(s_c) (computed; its error, like that of every
+// computed distance here, is < 1e-7 m at Earth radius).  Moving the particle
+// by delta changes each distance by at most delta, so for |p - p0| < (g -
+// 0.01 m) / 2 every neighbour stays farther than c by more than rounding and
+// the reference's argmin keeps c with the same candidate list: the caller
+// skips the walk inside that ball (anchor p0 = this position).  load_cell
+// sets the anchor to the cell centre with rs = (min_nb |c_nb - c|)/2 - 1 m,
+// the same argument at p0 = c.  A walk that changes cell leaves the anchor of
+// the new cell's load_cell.
 template <int MAXV>
-__device__ __forceinline__ int walk(const Cell<MAXV>& c, int cell, double x, double y, double z,
+__device__ __forceinline__ int walk(Cell<MAXV>& c, int cell, double x, double y, double z,
                                     const int* __restrict__ cellrec, const double4* __restrict__ cxyz, int C) {
     constexpr int REC = ((1 + 2 * MAXV) + 3) / 4 * 4;
     constexpr int Q0 = (1 + MAXV) / 4, Q1 = (2 * MAXV) / 4;  // int4 words holding cellsOnCell
@@ -539,7 +550,8 @@ __device__ __forceinline__ int walk(const Cell<MAXV>& c, int cell, double x, dou
         const double dx = q.x - x, dy = q.y - y, dz = q.z - z;
         s[k] = dx * dx + dy * dy + dz * dz;  // len3(q - p) before its sqrt
     }
-    const double ex = c.cx - x, ey = c.cy - y, ez = c.cz - z;  // c itself (cached centre)
+    const double4 qc = cxyz[cell];  // c itself, listed last
+    const double ex = qc.x - x, ey = qc.y - y, ez = qc.z - z;
     const double sc = ex * ex + ey * ey + ez * ez;
     const double inf = __builtin_huge_val();
     double bs = inf;
@@ -557,7 +569,19 @@ __device__ __forceinline__ int walk(const Cell<MAXV>& c, int cell, double x, dou
             if (s[k] == bs || sqrt(s[k]) == sqrt(bs)) return id[k];
         }
     }
-    return cell;  // c attains the minimum and no earlier candidate ties it
+    // c attains the minimum and no neighbour ties it (so every finite s_k > s_c)
+    double s2 = inf;
+#pragma unroll
+    for (int k = 0; k < MAXV; ++k)
+        if (ok[k] && s[k] < s2) s2 = s[k];
+    if (!(s2 < inf)) {
+        c.rs2 = inf;  // no neighbour with a finite distance: the walk can only keep c
+    } else {
+        const double ra = (sqrt(s2) - sqrt(sc) - 0.01) * 0.5;
+        c.rs2 = (ra > 0.0) ? ra * ra * (1.0 - 1e-9) : -1.0;
+    }
+    c.cx = x; c.cy = y; c.cz = z;
+    return cell;
 }
 
 template <int MAXV>
@@ -824,10 +848,9 @@ __global__ void __launch_bounds__(kTrajBlock, (TrajWaves<MAXV, PATH, EULER>::val
         } else {  // one-hop nearest-centre walk (:902-922)
             if (cell < 0 || cell >= C) { died = (int)step; break; }
             if (c.id != cell) dev::load_cell<MAXV, RCache<MAXV, PATH, EULER>::value>(c, cell, a.cellrec, a.vxyz, a.mono0, a.mono1, a.cxyz, a.cellB);
-            // Exact shortcut: if |p - c| < rs (half the distance to the nearest
-            // neighbour centre, minus 1 m), every neighbour is strictly farther
-            // than the current centre by far more than rounding, so the
-            // reference's argmin (current cell listed last, strict <) keeps c.
+            // Exact shortcut: inside the stay ball around the anchor every
+            // neighbour is strictly farther than c by more than rounding, so
+            // the reference's argmin (c listed last, strict <) keeps c (dev::walk).
             const double ex = x - c.cx, ey = y - c.cy, ez = z - c.cz;
             if (!(ex * ex + ey * ey + ez * ez < c.rs2)) {
                 cell = dev::walk<MAXV>(c, cell, x, y, z, a.cellrec, a.cxyz, C);
