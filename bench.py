@@ -12,6 +12,17 @@ over xGMI on a side stream, overlapped with the next segment's kernel.
 ``--config 3``: BASELINE configs[2] -- 1e7 particles/GPU, layer 10, dt 60 s,
 7-day pathline as 7 chained daily snapshot pairs (mops_amd/chain.py).
 
+``--config 4``: BASELINE configs[3] -- oRRS18to6-class mesh (3.5M ocean cells,
+80 levels), 1e7 particles in total sharded over the ranks (strong scaling),
+depth 20 m, dt 120 s, 30-day pathline over 31 daily snapshots that are
+generated and derived in HBM inside the timed region (2 fields resident,
+~75 GB each), RCCL all-gather of the continuation points per pair.
+
+``--config 5``: BASELINE configs[4] -- same mesh, 1.25e7 Gaussian-seeded
+(Gulf-of-Mexico box) particles per GPU (weak scaling, 1e8 on 8 GPUs), dt 60 s,
+monthly snapshots; ``--pairs`` monthly pairs of the 365-day run (default 1 =
+a 30-day sample of the 12, stated in the JSON).
+
 Inputs (mesh, fields, seeds) are resident in HBM before the timed region.
 Rank 0 prints one JSON line (driver contract).
 """
@@ -47,10 +58,13 @@ def parse():
     p.add_argument("--method", choices=["euler", "rk4"], default="euler")
     p.add_argument("--mode", choices=["streamline", "pathline"], default="streamline",
                    help="pathline: two snapshots (front/back), BASELINE config 3 shape")
-    p.add_argument("--config", type=int, choices=[2, 3], default=2,
+    p.add_argument("--config", type=int, choices=[2, 3, 4, 5], default=2,
                    help="BASELINE.json config: 2 = 1e6-particle 1-day streamline (default); 3 = 1e7-particle "
-                        "7-day chained pathline at layer 10, dt 60 s")
-    p.add_argument("--pairs", type=int, default=7, help="config 3: snapshot pairs (days)")
+                        "7-day chained pathline at layer 10, dt 60 s; 4 = oRRS18to6-class 1e7-particle 30-day "
+                        "pathline (strong scaling); 5 = oRRS18to6-class 1.25e7 Gaussian particles/GPU, monthly "
+                        "pairs (weak scaling)")
+    p.add_argument("--pairs", type=int, default=None,
+                   help="configs 3/4/5: snapshot pairs (defaults 7 daily / 30 daily / 1 monthly of 12)")
     p.add_argument("--backend", choices=["nccl", "gloo"], default="nccl",
                    help="collective backend for N > 1 (nccl = RCCL over xGMI; gloo only to rehearse the multi-rank "
                         "path on one GPU with MOPS_BENCH_ONE_DEVICE=1)")
@@ -78,6 +92,21 @@ def make_seeds(n: int, rank: int) -> np.ndarray:
     return seeds[~synth._land_mask(lat, lon, "continents")][:n]
 
 
+def make_gaussian_seeds(n: int, rank: int) -> np.ndarray:
+    """Config 5: truncated Gaussian in the Gulf-of-Mexico box, ocean only; one draw per rank."""
+    from mops_amd import synth
+    out = []
+    have = 0
+    k = 0
+    while have < n:
+        s = synth.gaussian_box_seeds(int((n - have) * 1.6) + 64, seed=2024 + 1000 * rank + k)
+        r = np.linalg.norm(s, axis=1)
+        lat = np.arcsin(s[:, 2] / r); lon = np.arctan2(s[:, 1], s[:, 0])
+        s = s[~synth._land_mask(lat, lon, "continents")]
+        out.append(s); have += len(s); k += 1
+    return np.concatenate(out)[:n]
+
+
 def measured_traffic(key: str, avg_kernel_s: float):
     """Per-launch DRAM bytes from the committed PMC summary (tools/make_traffic.py), if it is for this workload."""
     pmc_path = os.path.join(ROOT, "profiles", "pmc_traffic.json")
@@ -101,6 +130,12 @@ def algorithmic_bytes_per_pstep(nv: float, L: int, S: int = 1) -> float:
 
 
 CONFIG3 = dict(mode="pathline", particles=10_000_000, dt=60, duration=86400, record=3600, method="euler")
+# oRRS18to6 class: frequency-608 icosahedral dual (3.7M cells, 3.5M after the land cull), 80 levels
+CONFIG4 = dict(mode="pathline", particles=10_000_000, dt=120, duration=86400, record=3600, method="euler",
+               depth=20.0, freq=608, levels=80)
+CONFIG5 = dict(mode="pathline", particles=12_500_000, dt=60, duration=30 * 86400, record=30 * 86400,
+               method="euler", depth=20.0, freq=608, levels=80)
+PAIRS_DEFAULT = {3: 7, 4: 30, 5: 1}
 
 
 def layer_mid_depth(mesh, layer: int = 10) -> float:
@@ -110,12 +145,14 @@ def layer_mid_depth(mesh, layer: int = 10) -> float:
 
 def main():
     args = parse()
-    if args.config == 3:  # config-3 values for every option left at its config-2 default
+    if args.config in (3, 4, 5):  # config values for every option left at its config-2 default
         d = vars(argparse.Namespace(mode="streamline", particles=1_000_000, dt=120, duration=86400, record=3600,
-                                    method="euler"))
-        for k, v in CONFIG3.items():
+                                    method="euler", depth=800.0, freq=158, levels=60))
+        for k, v in {3: CONFIG3, 4: CONFIG4, 5: CONFIG5}[args.config].items():
             if getattr(args, k) == d[k]:
                 setattr(args, k, v)
+        if args.pairs is None:
+            args.pairs = PAIRS_DEFAULT[args.config]
     import torch
     import torch.distributed as dist
 
@@ -138,6 +175,7 @@ def main():
     mesh = synth.make_mesh(args.freq, n_levels=args.levels)
     if args.config == 3:
         args.depth = layer_mid_depth(mesh, 10)
+    if args.config in (3, 4, 5):
         return main_chain(args, mesh, dev, world, rank)
     snap = synth.make_snapshot(mesh, timestep=0)
     dmesh = DeviceMesh.from_mesh(mesh)
@@ -281,10 +319,13 @@ def main():
 
 
 def main_chain(args, mesh, dev, world, rank):
-    """BASELINE config 3: 1e7 particles/GPU, "layer 10", dt 60 s, 7-day pathline as 7 chained daily snapshot
-    pairs (MOPSPathline.run semantics, mops_amd/chain.py).  All 8 derived snapshots are resident in HBM before
-    the timed region; one bench step = the whole 7-day chain (seed locate per pair, 10 080 steps, per-pair line
-    assembly on device, an RCCL all-gather of each pair's continuation points when N > 1)."""
+    """BASELINE configs 3-5: chained snapshot-pair pathlines (MOPSPathline.run semantics, mops_amd/chain.py).
+
+    config 3: 1e7 particles/GPU, "layer 10", dt 60 s, 7 daily pairs; all 8 derived snapshots are resident in
+    HBM before the timed region.  configs 4/5: oRRS18to6-class mesh; each snapshot is generated and derived in
+    HBM inside the timed region (mops_field_create_device), two fields resident.  One bench step = the whole
+    chain (seed locate per pair, every integration step, per-pair line assembly on device, an RCCL all-gather
+    of each pair's continuation points when N > 1)."""
     import torch
     import torch.distributed as dist
     from mops_amd import synth
@@ -292,25 +333,52 @@ def main_chain(args, mesh, dev, world, rank):
     from mops_amd.engine import DeviceField, DeviceMesh
 
     n_snap = args.pairs + 1
-    snaps = [synth.make_snapshot(mesh, timestep=t, phase=0.35 * t) for t in range(n_snap)]
     dmesh = DeviceMesh.from_mesh(mesh)
-    fields = [DeviceField.from_snapshot(dmesh, s) for s in snaps]
-    seeds = make_seeds(args.particles, rank)
+    snaps = None
+    if args.config == 3:
+        snaps = [synth.make_snapshot(mesh, timestep=t, phase=0.35 * t) for t in range(n_snap)]
+        fields = [DeviceField.from_snapshot(dmesh, s) for s in snaps]
+        chain = PathlineChain(dmesh, lambda i, stream: fields[i], n_snap, gap_seconds=args.duration, device=dev,
+                              own_fields=False)
+    else:
+        from mops_amd.synth_device import DeviceFieldRecycler, DeviceSnapshotSource
+        src = DeviceSnapshotSource(mesh, dev)
+        chain = PathlineChain(dmesh, DeviceFieldRecycler(dmesh, src), n_snap, gap_seconds=args.duration,
+                              device=dev, own_fields=True, prefetch=False)
+    if args.config == 4:  # strong scaling: 1e7 particles in total, one contiguous shard per rank
+        allseeds = make_seeds(args.particles, 0)
+        lo, hi = len(allseeds) * rank // world, len(allseeds) * (rank + 1) // world
+        seeds = allseeds[lo:hi]
+        del allseeds
+    elif args.config == 5:
+        seeds = make_gaussian_seeds(args.particles, rank)
+    else:
+        seeds = make_seeds(args.particles, rank)
     n = seeds.shape[0]
-    chain = PathlineChain(dmesh, lambda i, stream: fields[i], n_snap, gap_seconds=args.duration, device=dev,
-                          own_fields=False)
     compute = torch.cuda.Stream(dev)
     comm = torch.cuda.Stream(dev)
-    gathered = torch.empty((world, n, 3), dtype=torch.float64, device=dev) if world > 1 else None
+    n_pad = n
+    if world > 1:  # equal-size all-gather buffers (config-4 shards may differ by one particle)
+        t = torch.tensor([n], dtype=torch.int64, device=dev if args.backend == "nccl" else "cpu")
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        n_pad = int(t.item())
+    gathered = torch.empty((world, n_pad, 3), dtype=torch.float64, device=dev) if world > 1 else None
+    send = torch.zeros((n_pad, 3), dtype=torch.float64, device=dev) if world > 1 else None
     timing = []
 
+    t_start = [time.perf_counter()]
+
     def on_pair(p, last):
+        if rank == 0 and args.pairs > 7:  # progress for long chains (stderr)
+            print(f"[bench] pair {p + 1}/{args.pairs} enqueued at {time.perf_counter() - t_start[0]:.1f} s",
+                  file=sys.stderr, flush=True)
         if world > 1:  # checkpoint: every rank gets the continuation points of all shards
             done = torch.cuda.Event(); done.record(compute)
             comm.wait_event(done)
             last.record_stream(comm)
             with torch.cuda.stream(comm):
-                all_gather_flat(dist, gathered.view(-1), last.view(-1), args.backend)
+                send[:n].copy_(last)
+                all_gather_flat(dist, gathered.view(-1), send.view(-1), args.backend)
 
     def one_call(timed):
         res = chain.run(seeds, depth=args.depth, method=1 if args.method == "euler" else 0, delta_t=args.dt,
@@ -349,20 +417,36 @@ def main_chain(args, mesh, dev, world, rank):
     launches_per_call = len(timing) / args.steps
     psteps_per_launch = attempted / args.steps / launches_per_call
     achieved = B * psteps_per_launch / avg_kernel_s / 1e9
-    traffic, measured = measured_traffic(f"ec30to60_chain_{args.method}_{args.particles}", avg_kernel_s)
+    mesh_class = "EC30to60" if args.config == 3 else "oRRS18to6"
+    traffic, measured = measured_traffic(f"{mesh_class.lower()}_chain{args.config}_{args.method}_{args.particles}",
+                                         avg_kernel_s)
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         seed_cells = dmesh_locate_host(dmesh, seeds, dev)
+        if snaps is None:  # configs 4/5: the first pair's snapshots, built on the host for the oracle
+            snaps = [synth.make_snapshot(mesh, timestep=t, phase=0.35 * t) for t in range(2)]
         cpu = cpu_baseline(mesh, snaps[0], snaps[1], seeds, seed_cells, args, args.duration // args.dt)
+    if args.config == 3:
+        workload = (f"EC30to60-class chained pathline (BASELINE config 3), {n:.0e} particles/GPU, layer 10 "
+                    f"({args.depth:.1f} m), dt {args.dt} s, {args.pairs} days = {args.pairs} daily pairs")
+    elif args.config == 4:
+        workload = (f"oRRS18to6-class chained pathline (BASELINE config 4), {int(n_all):.0e} particles in total "
+                    f"({n} on this rank), depth {args.depth:g} m, dt {args.dt} s, {args.pairs} days = {args.pairs} "
+                    "daily pairs, snapshots generated + derived in HBM inside the timed region")
+    else:
+        workload = (f"oRRS18to6-class chained pathline (BASELINE config 5), {n:.3g} Gaussian Gulf-of-Mexico particles"
+                    f"/GPU, depth {args.depth:g} m, dt {args.dt} s, {args.pairs} monthly pair(s) of the 12 in the "
+                    "365-day run (a bounded sample; every pair is the same work shape), snapshots generated + "
+                    "derived in HBM inside the timed region")
     if rank == 0:
         print(json.dumps({
             "metric": "particle-steps/sec", "value": value, "unit": "particle-steps/s", "n_gpus": world,
             "steps": args.steps, "warmup": args.warmup, "ms_per_step": elapsed / args.steps * 1e3,
-            "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "f64",
-            "data": "synthetic (icosahedral-dual Voronoi mesh, analytic flow phase-shifted per daily snapshot)",
+            "higher_is_better": True, "scaling": "strong" if args.config == 4 else "weak", "vs_baseline": None,
+            "dtype": "f64",
+            "data": "synthetic (icosahedral-dual Voronoi mesh, analytic flow phase-shifted per snapshot)",
             "config": {
-                "workload": (f"EC30to60-class chained pathline (BASELINE config 3), {n:.0e} particles/GPU, layer 10 "
-                             f"({args.depth:.1f} m), dt {args.dt} s, {args.pairs} days = {args.pairs} daily pairs"),
+                "workload": workload,
                 "cells": mesh.nCells, "vertices": mesh.nVertices, "levels": mesh.nVertLevels,
                 "particles_per_gpu": n, "particles_total": int(n_all), "integration_steps": n_steps,
                 "records_per_pair": args.duration // args.record, "method": args.method,

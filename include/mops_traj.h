@@ -115,6 +115,21 @@ int64_t mops_mesh_bytes(const mops_mesh* mesh);
  * CalcCellVertexVelocity (:270-318), CalcCellVertexVertVelocity (:320-366). */
 mops_status mops_field_create(const mops_mesh* mesh, const mops_snapshot_desc* desc, void* stream,
                               mops_field** out);
+/* As mops_field_create, but every array pointer in d_desc is a DEVICE pointer
+ * (raw fields already in HBM, e.g. decoded or generated on the GPU); they are
+ * read in place and stay owned by the caller.  Same preprocessing chain
+ * (MOPSApp::addSol, src/Core/MOPSApp.cpp:100-129); lets a snapshot-chaining
+ * driver (tutorial/pathLine.cpp:244-309) stream snapshots without a host
+ * round trip. */
+mops_status mops_field_create_device(const mops_mesh* mesh, const mops_snapshot_desc* d_desc, void* stream,
+                                     mops_field** out);
+/* Re-derive a field made by mops_field_create_device from another snapshot's
+ * raw DEVICE arrays, in place: no allocation, asynchronous on `stream`.  The
+ * reference rebuilds MPASOSolution per snapshot (MOPSApp::addSol); here a
+ * pair-chaining driver recycles the buffers of the snapshot it just finished
+ * (stream order: every earlier trajectory launch reading `field` on `stream`
+ * completes first).  The raw arrays must stay valid until the work runs. */
+mops_status mops_field_rebuild_device(mops_field* field, const mops_snapshot_desc* d_desc, void* stream);
 /* Upload already-derived vertex arrays (cellVertexZTop_vec [V*L],
  * cellVertexVelocity_vec [V*L*3], cellVertexVertVelocity_vec [V*(L+1)]);
  * the path MOPSApp::addSol takes when they are pre-set (MOPSApp.cpp:100,107,117). */

@@ -16,7 +16,7 @@ LIB_PATH = os.path.join(_HERE, "lib", "libmops_traj.so")
 EXPORTED = (
     "mops_last_error", "mops_abi_version",
     "mops_mesh_create", "mops_mesh_destroy", "mops_mesh_bytes",
-    "mops_field_create", "mops_field_create_derived", "mops_field_export", "mops_cell_to_vertex_attr",
+    "mops_field_create", "mops_field_create_device", "mops_field_rebuild_device", "mops_field_create_derived", "mops_field_export", "mops_cell_to_vertex_attr",
     "mops_field_destroy", "mops_field_bytes",
     "mops_locate_cells", "mops_order_particles",
     "mops_traj_num_records", "mops_traj_num_steps", "mops_traj_advance", "mops_traj_finalize",
@@ -90,6 +90,8 @@ def load(path: str | None = None):
     lib.mops_mesh_destroy.argtypes = [P]; lib.mops_mesh_destroy.restype = None
     lib.mops_mesh_bytes.argtypes = [P]; lib.mops_mesh_bytes.restype = I64
     lib.mops_field_create.argtypes = [P, P, P, P]; lib.mops_field_create.restype = st
+    lib.mops_field_create_device.argtypes = [P, P, P, P]; lib.mops_field_create_device.restype = st
+    lib.mops_field_rebuild_device.argtypes = [P, P, P]; lib.mops_field_rebuild_device.restype = st
     lib.mops_field_create_derived.argtypes = [P, P, P, P, P, P]; lib.mops_field_create_derived.restype = st
     lib.mops_field_export.argtypes = [P, P, P, P, P]; lib.mops_field_export.restype = st
     lib.mops_cell_to_vertex_attr.argtypes = [P, P, P, P]; lib.mops_cell_to_vertex_attr.restype = st

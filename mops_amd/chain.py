@@ -32,10 +32,17 @@ EARTH_RADIUS_M = 6_371_000.0  # pyMOPSAPI.py:46
 
 class PathlineChain:
     def __init__(self, mesh: DeviceMesh, make_field, n_snapshots: int, gap_seconds: int, device=None,
-                 own_fields: bool = True):
+                 own_fields: bool = True, prefetch: bool = True):
         """``make_field(i, stream) -> DeviceField`` builds snapshot i's field on ``stream``.
         With ``own_fields`` False the fields are the caller's (e.g. all resident
-        before a timed region) and are neither freed nor rebuilt here."""
+        before a timed region) and are neither freed nor rebuilt here.
+        ``prefetch`` builds snapshot p+2 on a side stream while pair p runs (3
+        fields resident); without it, p+2 is built after pair p has freed
+        snapshot p (2 resident: an oRRS18to6-class field at L=80 is ~75 GB).
+        Without prefetch, a ``make_field`` with ``refill(field, i, stream)``
+        (and optionally ``prepare(i)``, e.g. synth_device.DeviceFieldRecycler)
+        re-derives snapshot p's buffers in place as p+2 instead -- no
+        allocation and no host synchronisation between pairs."""
         if n_snapshots < 2:
             raise ValueError("a pathline chain needs at least two snapshots")
         self.mesh = mesh
@@ -44,6 +51,7 @@ class PathlineChain:
         self.gap = int(gap_seconds)
         self.device = device
         self.own_fields = own_fields
+        self.prefetch = prefetch
 
     def run(self, seeds, depth: float, particle_depths=None, method: int = L.MOPS_EULER, delta_t: int = 60,
             record_t: int = 360, direction: int = L.MOPS_FORWARD, follow_last: bool = True, keep_lines: bool = True,
@@ -77,7 +85,10 @@ class PathlineChain:
         pts_acc, vel_acc, tmp_acc, sal_acc = [], [], [], []
         last = None
         attempted = torch.zeros((), dtype=torch.int64, device=dev)
+        recycle = self.own_fields and not self.prefetch and hasattr(self.make_field, "refill")
         for p in range(self.n_snapshots - 1):
+            if recycle and p + 2 < self.n_snapshots and hasattr(self.make_field, "prepare"):
+                self.make_field.prepare(p + 2)  # raw snapshot p+2 generated on a side stream during pair p
             with torch.cuda.stream(cs):
                 if p == 0 or not follow_last:
                     s = seeds0
@@ -111,8 +122,12 @@ class PathlineChain:
                     tmp_acc.append(out["temperature"][:, sl]); sal_acc.append(out["salinity"][:, sl])
             if on_pair is not None:
                 on_pair(p, last)
+            if recycle:  # re-derive snapshot p's buffers as snapshot p+2, stream-ordered after pair p
+                if p + 2 < self.n_snapshots:
+                    fields[p + 2] = self.make_field.refill(fields.pop(p), p + 2, cs)
+                continue
             # overlap: build the field pair p+1 will need while pair p computes
-            if p + 2 < self.n_snapshots:
+            if p + 2 < self.n_snapshots and (self.prefetch or not self.own_fields):
                 if self.own_fields:
                     with torch.cuda.stream(side):
                         fields[p + 2] = self.make_field(p + 2, side.cuda_stream)
@@ -123,7 +138,11 @@ class PathlineChain:
             if self.own_fields:
                 cs.synchronize()  # pair p finished with `done` before it is freed
                 done.close()
+                if p + 2 < self.n_snapshots and not self.prefetch:
+                    with torch.cuda.stream(cs):
+                        fields[p + 2] = self.make_field(p + 2, cs.cuda_stream)
         if self.own_fields:
+            cs.synchronize()
             for f in fields.values():
                 f.close()
         res = dict(lastPoint=last, death_step=ps.original(ps.death), attempted=attempted)

@@ -103,6 +103,10 @@ struct mops_field {
     // 96-B, 16-B-aligned read gives a vertex's whole contribution when the
     // particle sits in layer k
     double* d_pr = nullptr;
+    // derivation intermediates (cell zTop [C][L], cell-centre xyz velocity [C][L][3]), kept
+    // only by fields built from device arrays so mops_field_rebuild_device never allocates
+    double* d_ztc = nullptr;
+    double* d_velc = nullptr;
     int64_t bytes = 0;
 };
 
@@ -1371,6 +1375,7 @@ void free_field(mops_field* f) {
     if (!f) return;
     (void)hipFree(f->d_zt); (void)hipFree(f->d_vel); (void)hipFree(f->d_w); (void)hipFree(f->d_mono);
     (void)hipFree(f->d_pr);
+    (void)hipFree(f->d_ztc); (void)hipFree(f->d_velc);
     delete f;
 }
 
@@ -1548,11 +1553,11 @@ int64_t mops_mesh_bytes(const mops_mesh* mesh) { return mesh ? mesh->bytes : 0; 
 static mops_status compute_mono(const mops_mesh* mesh, mops_field* f, hipStream_t s) {
     const int64_t npr = mesh->V * (int64_t)std::max(mesh->L - 1, 0);
     // + one all-zero record at index npr: pair_sums reads it for v >= nv
-    MOPS_TRY(dmalloc(&f->d_pr, (size_t)((npr + 1) * 12), &f->bytes));
+    if (!f->d_pr) MOPS_TRY(dmalloc(&f->d_pr, (size_t)((npr + 1) * 12), &f->bytes));
     HIP_TRY(hipMemsetAsync(f->d_pr + npr * 12, 0, 12 * sizeof(double), s));
     if (npr > 0)
         pair_record_kernel<<<grid_for(npr), kBlock, 0, s>>>(mesh->V, mesh->L, f->d_zt, f->d_vel, f->d_w, f->d_pr);
-    MOPS_TRY(dmalloc(&f->d_mono, (size_t)mesh->C, &f->bytes));
+    if (!f->d_mono) MOPS_TRY(dmalloc(&f->d_mono, (size_t)mesh->C, &f->bytes));
     mono_kernel<<<grid_for(mesh->C), kBlock, 0, s>>>(mesh->C, mesh->maxv, mesh->rec_ints, mesh->d_cellrec, f->d_zt,
                                                     mesh->L, f->d_mono);
     HIP_TRY(hipGetLastError());
@@ -1582,64 +1587,121 @@ mops_status mops_field_create_derived(const mops_mesh* mesh, const double* h_zt,
     return MOPS_OK;
 }
 
+static mops_status field_create_impl(const mops_mesh* mesh, const mops_snapshot_desc* desc, bool on_device,
+                                     hipStream_t s, mops_field** out);
+static mops_status field_derive(const mops_mesh* mesh, mops_field* f, const mops_snapshot_desc* d, double* ztc,
+                                double* velc, hipStream_t s);
+
 mops_status mops_field_create(const mops_mesh* mesh, const mops_snapshot_desc* desc, void* stream,
                               mops_field** out) {
-    if (!mesh || !desc || !out) return fail(MOPS_ERR_INVALID, "mops_field_create: null argument");
-    *out = nullptr;
+    return field_create_impl(mesh, desc, false, (hipStream_t)stream, out);
+}
+
+mops_status mops_field_create_device(const mops_mesh* mesh, const mops_snapshot_desc* d_desc, void* stream,
+                                     mops_field** out) {
+    return field_create_impl(mesh, d_desc, true, (hipStream_t)stream, out);
+}
+
+mops_status mops_field_rebuild_device(mops_field* field, const mops_snapshot_desc* d_desc, void* stream) {
+    if (!field || !d_desc || !field->mesh) return fail(MOPS_ERR_INVALID, "mops_field_rebuild_device: null argument");
+    if (!field->d_ztc || !field->d_velc)
+        return fail(MOPS_ERR_INVALID, "mops_field_rebuild_device: field was not created by mops_field_create_device");
+    return field_derive(field->mesh, field, d_desc, field->d_ztc, field->d_velc, (hipStream_t)stream);
+}
+
+}  // extern "C"
+
+static mops_status check_snapshot(const mops_mesh* mesh, const mops_snapshot_desc* desc) {
     if (!desc->h_layer_thickness)
         return fail(MOPS_ERR_INVALID, "cellLayerThickness is not defined");  // MPASOSolution.cpp:540-544
     if (!desc->h_zonal_velocity || !desc->h_meridional_velocity)
         return fail(MOPS_ERR_INVALID, "zonal/meridional velocity required");
     if (!mesh->d_cov) return fail(MOPS_ERR_INVALID, "mesh has no cellsOnVertex");
-    hipStream_t s = (hipStream_t)stream;
+    return MOPS_OK;
+}
+
+// Enqueue the derivation chain (MOPSApp::addSol: calcCellCenterZtop, CalcCellVertexZtop,
+// CalcCellCenterVelocityByZM, CalcCellVertexVelocity, CalcCellVertexVertVelocity, then the
+// engine's level-pair records and monotone flags) from raw DEVICE arrays `d` into f,
+// allocating only the buffers f does not have yet.  Asynchronous on s.
+static mops_status field_derive(const mops_mesh* mesh, mops_field* f, const mops_snapshot_desc* d, double* ztc,
+                                double* velc, hipStream_t s) {
+    MOPS_TRY(check_snapshot(mesh, d));
     const int64_t C = mesh->C, V = mesh->V;
     const int L = mesh->L;
+    const double* bot = d->h_bottom_depth;
+    const double* ssh = bot ? nullptr : d->h_surface_height;
+    if (!f->d_zt) MOPS_TRY(dmalloc(&f->d_zt, (size_t)(V * L), &f->bytes));
+    if (!f->d_vel) MOPS_TRY(dmalloc(&f->d_vel, (size_t)(V * L * 3), &f->bytes));
+    if (!f->d_w) MOPS_TRY(dmalloc(&f->d_w, (size_t)(V * (L + 1)), &f->bytes));
+    cell_ztop_kernel<<<grid_for(C), kBlock, 0, s>>>(C, L, d->h_layer_thickness, bot, ssh, ztc);
+    cell_to_vertex_kernel<1><<<grid_for(V * L), kBlock, 0, s>>>(V, L, mesh->d_cov, mesh->d_cxyz, mesh->d_vxyz, ztc,
+                                                               f->d_zt, 0);
+    center_vel_zm_kernel<<<grid_for(C * L), kBlock, 0, s>>>(C, L, mesh->d_cxyz, d->h_zonal_velocity,
+                                                            d->h_meridional_velocity, velc);
+    cell_to_vertex_kernel<3><<<grid_for(V * L), kBlock, 0, s>>>(V, L, mesh->d_cov, mesh->d_cxyz, mesh->d_vxyz, velc,
+                                                               f->d_vel, 0);
+    if (d->h_vert_velocity_top) {
+        cell_to_vertex_kernel<1><<<grid_for(V * (L + 1)), kBlock, 0, s>>>(V, L + 1, mesh->d_cov, mesh->d_cxyz,
+                                                                         mesh->d_vxyz, d->h_vert_velocity_top,
+                                                                         f->d_w, 0);
+    } else {
+        HIP_TRY(hipMemsetAsync(f->d_w, 0, (size_t)(V * (L + 1)) * sizeof(double), s));
+    }
+    MOPS_TRY(compute_mono(mesh, f, s));
+    HIP_TRY(hipGetLastError());
+    return MOPS_OK;
+}
+
+// Raw inputs either uploaded from host (mops_field_create: staged, then freed) or
+// read in place from HBM (mops_field_create_device: nothing copied; the
+// intermediates are kept for mops_field_rebuild_device).
+static mops_status field_create_impl(const mops_mesh* mesh, const mops_snapshot_desc* desc, bool on_device,
+                                     hipStream_t s, mops_field** out) {
+    if (!mesh || !desc || !out) return fail(MOPS_ERR_INVALID, "mops_field_create: null argument");
+    *out = nullptr;
+    MOPS_TRY(check_snapshot(mesh, desc));
+    const int64_t C = mesh->C;
+    const int L = mesh->L;
     mops_field* f = new mops_field();
-    f->mesh = mesh; f->V = V; f->L = L;
+    f->mesh = mesh; f->V = mesh->V; f->L = L;
+    mops_snapshot_desc dd = *desc;  // device view of the raw arrays
     double *thick = nullptr, *bot = nullptr, *ssh = nullptr, *zon = nullptr, *mer = nullptr, *wc = nullptr;
     double *ztc = nullptr, *velc = nullptr;
     int64_t scratch = 0;
     mops_status st = MOPS_OK;
-    auto cleanup = [&]() {
-        (void)hipFree(thick); (void)hipFree(bot); (void)hipFree(ssh); (void)hipFree(zon); (void)hipFree(mer); (void)hipFree(wc); (void)hipFree(ztc);
-        (void)hipFree(velc);
-    };
     do {
-        if ((st = upload(desc->h_layer_thickness, (size_t)(C * L), &thick, &scratch, s)) != MOPS_OK) break;
-        if (desc->h_bottom_depth && (st = upload(desc->h_bottom_depth, (size_t)C, &bot, &scratch, s)) != MOPS_OK) break;
-        if (!desc->h_bottom_depth && desc->h_surface_height &&
-            (st = upload(desc->h_surface_height, (size_t)C, &ssh, &scratch, s)) != MOPS_OK) break;
-        if ((st = upload(desc->h_zonal_velocity, (size_t)(C * L), &zon, &scratch, s)) != MOPS_OK) break;
-        if ((st = upload(desc->h_meridional_velocity, (size_t)(C * L), &mer, &scratch, s)) != MOPS_OK) break;
-        if (desc->h_vert_velocity_top &&
-            (st = upload(desc->h_vert_velocity_top, (size_t)(C * (L + 1)), &wc, &scratch, s)) != MOPS_OK) break;
-        if ((st = dmalloc(&ztc, (size_t)(C * L), &scratch)) != MOPS_OK) break;
-        if ((st = dmalloc(&velc, (size_t)(C * L * 3), &scratch)) != MOPS_OK) break;
-        if ((st = dmalloc(&f->d_zt, (size_t)(V * L), &f->bytes)) != MOPS_OK) break;
-        if ((st = dmalloc(&f->d_vel, (size_t)(V * L * 3), &f->bytes)) != MOPS_OK) break;
-        if ((st = dmalloc(&f->d_w, (size_t)(V * (L + 1)), &f->bytes)) != MOPS_OK) break;
-        cell_ztop_kernel<<<grid_for(C), kBlock, 0, s>>>(C, L, thick, bot, ssh, ztc);
-        cell_to_vertex_kernel<1><<<grid_for(V * L), kBlock, 0, s>>>(V, L, mesh->d_cov, mesh->d_cxyz, mesh->d_vxyz, ztc,
-                                                                   f->d_zt, 0);
-        center_vel_zm_kernel<<<grid_for(C * L), kBlock, 0, s>>>(C, L, mesh->d_cxyz, zon, mer, velc);
-        cell_to_vertex_kernel<3><<<grid_for(V * L), kBlock, 0, s>>>(V, L, mesh->d_cov, mesh->d_cxyz, mesh->d_vxyz,
-                                                                   velc, f->d_vel, 0);
-        if (wc) {
-            cell_to_vertex_kernel<1><<<grid_for(V * (L + 1)), kBlock, 0, s>>>(V, L + 1, mesh->d_cov, mesh->d_cxyz,
-                                                                             mesh->d_vxyz, wc, f->d_w, 0);
-        } else {
-            (void)hipMemsetAsync(f->d_w, 0, (size_t)(V * (L + 1)) * sizeof(double), s);
+        if (!on_device) {
+            if ((st = upload(desc->h_layer_thickness, (size_t)(C * L), &thick, &scratch, s)) != MOPS_OK) break;
+            if (desc->h_bottom_depth && (st = upload(desc->h_bottom_depth, (size_t)C, &bot, &scratch, s)) != MOPS_OK)
+                break;
+            if (!desc->h_bottom_depth && desc->h_surface_height &&
+                (st = upload(desc->h_surface_height, (size_t)C, &ssh, &scratch, s)) != MOPS_OK) break;
+            if ((st = upload(desc->h_zonal_velocity, (size_t)(C * L), &zon, &scratch, s)) != MOPS_OK) break;
+            if ((st = upload(desc->h_meridional_velocity, (size_t)(C * L), &mer, &scratch, s)) != MOPS_OK) break;
+            if (desc->h_vert_velocity_top &&
+                (st = upload(desc->h_vert_velocity_top, (size_t)(C * (L + 1)), &wc, &scratch, s)) != MOPS_OK) break;
+            dd.h_layer_thickness = thick; dd.h_bottom_depth = bot; dd.h_surface_height = ssh;
+            dd.h_zonal_velocity = zon; dd.h_meridional_velocity = mer; dd.h_vert_velocity_top = wc;
         }
-        if ((st = compute_mono(mesh, f, s)) != MOPS_OK) break;
-        hipError_t e = hipGetLastError();
-        if (e == hipSuccess) e = hipStreamSynchronize(s);
+        if ((st = dmalloc(&ztc, (size_t)(C * L), on_device ? &f->bytes : &scratch)) != MOPS_OK) break;
+        if (on_device) f->d_ztc = ztc;  // owned by the field from here on
+        if ((st = dmalloc(&velc, (size_t)(C * L * 3), on_device ? &f->bytes : &scratch)) != MOPS_OK) break;
+        if (on_device) f->d_velc = velc;
+        if ((st = field_derive(mesh, f, &dd, ztc, velc, s)) != MOPS_OK) break;
+        hipError_t e = hipStreamSynchronize(s);
         if (e != hipSuccess) { st = fail(MOPS_ERR_HIP, std::string("preprocessing: ") + hipGetErrorString(e)); break; }
     } while (0);
-    cleanup();
+    if (!on_device) {
+        (void)hipFree(thick); (void)hipFree(bot); (void)hipFree(ssh); (void)hipFree(zon); (void)hipFree(mer);
+        (void)hipFree(wc); (void)hipFree(ztc); (void)hipFree(velc);
+    }
     if (st != MOPS_OK) { free_field(f); return st; }
     *out = f;
     return MOPS_OK;
 }
+
+extern "C" {
 
 mops_status mops_cell_to_vertex_attr(const mops_mesh* mesh, const double* d_cell_attr, double* d_vertex_attr,
                                      void* stream) {

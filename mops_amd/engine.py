@@ -126,6 +126,39 @@ class DeviceField:
                 "mops_field_create")
         return cls(mesh, h)
 
+    @staticmethod
+    def _device_desc(snap: dict, timestep: int):
+        def dp(k):
+            t = snap.get(k)
+            if t is None:
+                return None
+            if not (t.is_cuda and t.dtype.is_floating_point and t.element_size() == 8 and t.is_contiguous()):
+                raise ValueError(f"{k}: expected a contiguous float64 CUDA tensor")
+            return C.c_void_p(t.data_ptr())
+        return L.SnapshotDesc(int(timestep), dp("layerThickness"), dp("bottomDepth"), dp("surfaceHeight"),
+                              dp("zonalVelocity"), dp("meridionalVelocity"), dp("vertVelocityTop"))
+
+    @classmethod
+    def from_device_snapshot(cls, mesh: DeviceMesh, snap: dict, timestep: int = 0, stream=None):
+        """Raw fields already in HBM (float64 CUDA tensors keyed like synth.Snapshot:
+        layerThickness, bottomDepth, zonalVelocity, meridionalVelocity, vertVelocityTop;
+        optional surfaceHeight) -- mops_field_create_device, no host round trip.
+        Synchronises ``stream`` before returning."""
+        desc = cls._device_desc(snap, timestep)
+        h = C.c_void_p()
+        L.check(L.load().mops_field_create_device(mesh.handle, C.byref(desc), _stream_handle(stream), C.byref(h)),
+                "mops_field_create_device")
+        return cls(mesh, h)
+
+    def rebuild_from_device(self, snap: dict, timestep: int = 0, stream=None):
+        """Re-derive this field in place from another snapshot's HBM tensors
+        (mops_field_rebuild_device): asynchronous on ``stream``, stream-ordered
+        after every earlier launch that reads this field there."""
+        desc = self._device_desc(snap, timestep)
+        L.check(L.load().mops_field_rebuild_device(self.handle, C.byref(desc), _stream_handle(stream)),
+                "mops_field_rebuild_device")
+        return self
+
     @classmethod
     def from_derived(cls, mesh: DeviceMesh, vertex_ztop, vertex_vel, vertex_w=None, stream=None):
         lib = L.load()

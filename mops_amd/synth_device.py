@@ -1,0 +1,125 @@
+"""Synthetic snapshot fields generated directly in HBM.
+
+Same analytic flow as :func:`mops_amd.synth.make_snapshot` (solid body +
+travelling wave-3, depth decay, w on the interface grid), evaluated with torch
+on the GPU, so long pathline chains on oRRS18to6-class meshes (3.5M cells x
+80 levels: 2.2 GB per raw field) can stream dozens of daily snapshots through
+``mops_field_create_device`` without building them on the host.  Values agree
+with the numpy generator to rounding (libm vs device sin/cos); the parity
+tests use the numpy generator, this module only feeds the configs 4/5 bench.
+"""
+from __future__ import annotations
+
+import math
+
+import numpy as np
+
+
+class DeviceSnapshotSource:
+    """Per-mesh constants on the device; ``make(timestep, phase)`` returns the raw
+    MPASOSolution arrays of one snapshot as float64 CUDA tensors."""
+
+    def __init__(self, mesh, device, u0: float = 0.5, u1: float = 0.25, w0: float = 1.0e-5):
+        import torch
+        self.torch = torch
+        self.device = device
+        self.L = int(mesh.nVertLevels)
+        self.lat = torch.as_tensor(np.ascontiguousarray(mesh.lat_cell, dtype=np.float64), device=device)
+        self.lon = torch.as_tensor(np.ascontiguousarray(mesh.lon_cell, dtype=np.float64), device=device)
+        rbd = np.asarray(mesh.refBottomDepth, dtype=np.float64)
+        self.H = float(rbd[-1])
+        self.ref_dz = torch.as_tensor(np.diff(np.concatenate([[0.0], rbd])), device=device)
+        self.u0, self.u1, self.w0 = u0, u1, w0
+
+    def make(self, timestep: int = 0, phase: float = 0.0) -> dict:
+        torch = self.torch
+        lat, lon, H = self.lat, self.lon, self.H
+        bot = H - 0.5 * (H - 2000.0) * (1.0 + torch.sin(2.0 * lat) * torch.cos(3.0 * lon)) * 0.5
+        bot = torch.clamp(bot, 1500.0, H)
+        ssh = 0.5 * torch.cos(lat) * torch.sin(2.0 * lon + phase)
+        thick = self.ref_dz[None, :] * ((bot + ssh) / H)[:, None]
+        csum = torch.cumsum(thick, dim=1)
+        zmid = csum - 0.5 * thick
+        decay = torch.exp(-zmid / 1500.0)
+        del zmid
+        cl = torch.cos(lat)[:, None]
+        u = (self.u0 * cl + self.u1 * torch.cos(3.0 * lon - phase)[:, None] * torch.sin(2.0 * lat)[:, None] * cl) * decay
+        v = (self.u1 * torch.sin(3.0 * lon - phase)[:, None] * cl * cl) * decay
+        del decay
+        zi = torch.cat([torch.zeros((lat.shape[0], 1), dtype=torch.float64, device=self.device), csum], dim=1)
+        del csum
+        wv = (self.w0 * torch.sin(2.0 * lat)[:, None] * torch.sin(math.pi * zi / zi[:, -1:])
+              * torch.cos(lon - phase)[:, None])
+        del zi
+        return {"layerThickness": thick.contiguous(), "bottomDepth": bot.contiguous(),
+                "zonalVelocity": u.contiguous(), "meridionalVelocity": v.contiguous(),
+                "vertVelocityTop": wv.contiguous(), "timestep": int(timestep)}
+
+
+class DeviceFieldRecycler:
+    """``make_field`` for :class:`mops_amd.chain.PathlineChain` with in-place refills.
+
+    * ``self(i, stream)`` creates a field (chain start: snapshots 0 and 1);
+    * ``prepare(i)`` generates snapshot i's raw arrays on a side stream, so it
+      overlaps the running pair (one raw set, reused once its last reader is done);
+    * ``refill(field, i, stream)`` re-derives the finished pair's field in place
+      from them (mops_field_rebuild_device): no allocation, no host sync.
+    """
+
+    def __init__(self, dmesh, source: DeviceSnapshotSource, phase_per_snapshot: float = 0.35):
+        torch = source.torch
+        self.torch = torch
+        self.dmesh = dmesh
+        self.source = source
+        self.phase = phase_per_snapshot
+        self.side = torch.cuda.Stream(device=source.device)
+        self.raw = None
+        self.raw_i = None
+        self.ready = None
+        self.consumed = None
+
+    def __call__(self, i, stream):
+        from .engine import DeviceField
+        torch = self.torch
+        snap = self.source.make(timestep=i, phase=self.phase * i)
+        torch.cuda.current_stream(self.source.device).synchronize()
+        f = DeviceField.from_device_snapshot(self.dmesh, snap, timestep=i, stream=stream)
+        del snap
+        return f
+
+    def prepare(self, i):
+        torch = self.torch
+        with torch.cuda.stream(self.side):
+            if self.consumed is not None:
+                self.side.wait_event(self.consumed)  # the previous refill has read the raw set
+            self.raw = None
+            self.raw = self.source.make(timestep=i, phase=self.phase * i)
+            self.ready = torch.cuda.Event()
+            self.ready.record(self.side)
+            self.raw_i = i
+
+    def refill(self, field, i, stream):
+        """``stream``: the torch stream the chain computes on."""
+        torch = self.torch
+        if self.raw_i != i:
+            self.prepare(i)
+        stream.wait_event(self.ready)
+        field.rebuild_from_device(self.raw, timestep=i, stream=stream.cuda_stream)
+        self.consumed = torch.cuda.Event()
+        self.consumed.record(stream)
+        return field
+
+
+def device_field_factory(dmesh, source: DeviceSnapshotSource, phase_per_snapshot: float = 0.35):
+    """Plain ``make_field(i, stream)``: snapshot i generated and derived in HBM into a new field."""
+    from .engine import DeviceField
+    torch = source.torch
+
+    def make(i, stream):
+        snap = source.make(timestep=i, phase=phase_per_snapshot * i)
+        torch.cuda.current_stream(source.device).synchronize()  # generated before the engine reads it
+        f = DeviceField.from_device_snapshot(dmesh, snap, timestep=i, stream=stream)
+        del snap  # mops_field_create_device synchronises its stream before returning
+        torch.cuda.empty_cache()  # hand the raw-field blocks back: the engine allocates fields with hipMalloc
+        return f
+    return make

@@ -43,3 +43,61 @@ def test_chain_matches_oracle(engine_lib, oracle_lib, gpu, small_case, method, p
     assert got["points"].shape[1] == 7 + 6          # 6 records + seed, then 6 more records
     for k in ("points", "velocity", "temperature", "salinity", "lastPoint"):
         assert np.array_equal(got[k].cpu().numpy(), ref[k]), k
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("recycle", [False, True], ids=["fresh-fields", "recycled-fields"])
+def test_chain_two_resident_fields_from_device_snapshots(engine_lib, oracle_lib, gpu, small_case, recycle):
+    """The configs 4/5 chain policies: snapshots handed over as HBM tensors
+    (mops_field_create_device), two fields resident (prefetch=False), and either
+    a fresh field per snapshot or snapshot p's buffers re-derived in place as
+    p+2 (mops_field_rebuild_device) -- same lines as the oracle chain."""
+    import torch
+    from mops_amd import synth
+    from mops_amd.chain import PathlineChain
+    from mops_amd.engine import DeviceField, DeviceMesh
+    mesh, _, _ = small_case
+    snaps = [synth.make_snapshot(mesh, timestep=t, phase=0.35 * t) for t in range(5)]
+    dm = DeviceMesh.from_mesh(mesh)
+    keys = ("layerThickness", "bottomDepth", "zonalVelocity", "meridionalVelocity", "vertVelocityTop")
+    keep = []
+
+    def raw(i):
+        d = {k: torch.as_tensor(getattr(snaps[i], k), device="cuda") for k in keys}
+        keep.append(d)
+        return d
+
+    class Make:
+        def __call__(self, i, stream):
+            d = raw(i)
+            torch.cuda.current_stream().synchronize()
+            return DeviceField.from_device_snapshot(dm, d, timestep=i, stream=stream)
+
+    class Recycle(Make):
+        def refill(self, field, i, stream):
+            d = raw(i)
+            stream.wait_stream(torch.cuda.current_stream())
+            return field.rebuild_from_device(d, timestep=i, stream=stream.cuda_stream)
+
+    seeds = synth.uniform_band_seeds(100, seed=9)
+    chain = PathlineChain(dm, Recycle() if recycle else Make(), len(snaps), gap_seconds=21600, prefetch=False)
+    got = chain.run(seeds, depth=250.0, method=1, delta_t=600, record_t=3600)
+    ref = oracle_chain(oracle_lib, mesh, snaps, seeds, 250.0, None, 21600, 600, 3600, euler=True)
+    for k in ("points", "velocity", "lastPoint"):
+        assert np.array_equal(got[k].cpu().numpy(), ref[k]), k
+
+
+@pytest.mark.gpu
+def test_device_snapshot_generator_matches_host(engine_lib, gpu, small_case):
+    """mops_amd.synth_device (configs 4/5 bench input) reproduces synth.make_snapshot to rounding."""
+    from mops_amd import synth
+    from mops_amd.synth_device import DeviceSnapshotSource
+    mesh, _, _ = small_case
+    src = DeviceSnapshotSource(mesh, "cuda")
+    d = src.make(timestep=2, phase=0.7)
+    h = synth.make_snapshot(mesh, timestep=2, phase=0.7)
+    for k in ("layerThickness", "bottomDepth", "zonalVelocity", "meridionalVelocity", "vertVelocityTop"):
+        a = d[k].cpu().numpy().reshape(-1)
+        b = getattr(h, k)
+        assert a.shape == b.shape, k
+        assert np.allclose(a, b, rtol=1e-12, atol=1e-15), k
