@@ -71,10 +71,14 @@ class PathlineChain:
                                depth=float(np.float32(depth)), direction=int(direction), method=int(method))
         if cfg.n_steps <= 0 or cfg.n_records <= 0:
             raise ValueError("invalid trajectory settings for a pair (deltaT/recordT vs the snapshot gap)")
-        seeds0 = torch.as_tensor(np.ascontiguousarray(seeds, dtype=np.float64).reshape(-1, 3), device=dev)
-        n = int(seeds0.shape[0])
-        per_particle = particle_depths is not None and len(particle_depths) == n
-        pdep = (torch.as_tensor(np.asarray(particle_depths, dtype=np.float32), device=dev) if per_particle else None)
+        # everything below is ordered on `cs` (the host never waits between pairs, so a
+        # tensor touched on another stream could be read before `cs` has written it)
+        with torch.cuda.stream(cs):
+            seeds0 = torch.as_tensor(np.ascontiguousarray(seeds, dtype=np.float64).reshape(-1, 3), device=dev)
+            n = int(seeds0.shape[0])
+            per_particle = particle_depths is not None and len(particle_depths) == n
+            pdep = (torch.as_tensor(np.asarray(particle_depths, dtype=np.float32), device=dev) if per_particle
+                    else None)
 
         fields = {}
         with torch.cuda.stream(cs):
@@ -145,10 +149,13 @@ class PathlineChain:
             cs.synchronize()
             for f in fields.values():
                 f.close()
-        res = dict(lastPoint=last, death_step=ps.original(ps.death), attempted=attempted)
-        if keep_lines:
-            res.update(points=torch.cat(pts_acc, 1), velocity=torch.cat(vel_acc, 1), temperature=torch.cat(tmp_acc, 1),
-                       salinity=torch.cat(sal_acc, 1))
+        with torch.cuda.stream(cs):
+            res = dict(lastPoint=last, death_step=ps.original(ps.death), attempted=attempted)
+            if keep_lines:
+                res.update(points=torch.cat(pts_acc, 1), velocity=torch.cat(vel_acc, 1),
+                           temperature=torch.cat(tmp_acc, 1), salinity=torch.cat(sal_acc, 1))
+        if cs != torch.cuda.current_stream(dev):
+            torch.cuda.current_stream(dev).wait_stream(cs)  # results are read on the caller's stream
         return res
 
 

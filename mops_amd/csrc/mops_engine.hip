@@ -63,6 +63,7 @@ constexpr int kBlock = 256;
 #define MOPS_TRAJ_BLOCK 64  // one wave per workgroup: a slow wave never holds a block's slots
 #endif
 constexpr int kTrajBlock = MOPS_TRAJ_BLOCK;
+constexpr int kPairRec = 10;  // doubles per level-pair record (see mops_field::d_pr)
 
 inline int rec_ints_for(int maxv) { return ((1 + 2 * maxv) + 3) / 4 * 4; }
 
@@ -98,10 +99,10 @@ struct mops_field {
     double* d_vel = nullptr;  // cellVertexVelocity [V][L][3]
     double* d_w = nullptr;    // cellVertexVertVelocity [V][L+1]
     uint8_t* d_mono = nullptr;  // [C] 1 = every vertex column of the cell strictly decreasing (margin)
-    // level-pair records [V][L-1][12] doubles, record k-1 of vertex v =
-    // {z_0, z_{k-1}, z_k, w_{k-1}, w_k, vel_{k-1} (3), vel_k (3), pad}: one
-    // 96-B, 16-B-aligned read gives a vertex's whole contribution when the
-    // particle sits in layer k
+    // level-pair records [V][L-1][kPairRec] doubles, record k-1 of vertex v =
+    // {z_{k-1}, z_k, w_{k-1}, w_k, vel_{k-1} (3), vel_k (3)}: one 80-B,
+    // 16-B-aligned read (5 x dwordx4) gives a vertex's whole contribution when
+    // the particle sits in layer k
     double* d_pr = nullptr;
     // derivation intermediates (cell zTop [C][L], cell-centre xyz velocity [C][L][3]), kept
     // only by fields built from device arrays so mops_field_rebuild_device never allocates
@@ -599,7 +600,7 @@ __device__ __forceinline__ bool weights_finite(const Cell<MAXV>& c, const double
 
 struct Field {
     const double* __restrict__ zt;   // cellVertexZTop [V][L]
-    const double* __restrict__ pr;   // level-pair records [V][L-1][12] (see mops_field)
+    const double* __restrict__ pr;   // level-pair records [V][L-1][kPairRec] (see mops_field)
 };
 
 // Weighted sums of one level-pair record per vertex: everything an
@@ -607,7 +608,7 @@ struct Field {
 // reference's vertex order, so every value equals its reference counterpart
 // (col(), TBBKernel::CalcVelocity, CalcAttribute) bit for bit.
 struct Pair {
-    double z0, zm, zk;   // z_0, z_{k-1}, z_k
+    double zm, zk;       // z_{k-1}, z_k
     double wm, wk;       // vertical velocity at interfaces k-1, k
     double um0, um1, um2, uk0, uk1, uk2;  // horizontal velocity at levels k-1, k
 };
@@ -624,31 +625,31 @@ struct Pair {
 template <int MAXV, int GR>
 __device__ __forceinline__ void pair_sums(const Cell<MAXV>& c, const double* w, const double* __restrict__ pr, int L,
                                           int k, Pair& S) {
-    S.z0 = S.zm = S.zk = S.wm = S.wk = 0.0;
+    S.zm = S.zk = S.wm = S.wk = 0.0;
     S.um0 = S.um1 = S.um2 = S.uk0 = S.uk1 = S.uk2 = 0.0;
     const int64_t zrec = (int64_t)c.V * (L - 1);
 #pragma unroll
     for (int v0 = 0; v0 < MAXV; v0 += GR) {
         if (v0 < c.nv) {
-            double2 a[GR][6];
+            double2 a[GR][kPairRec / 2];
 #pragma unroll
             for (int j = 0; j < GR; ++j) {
                 const int v = v0 + j;
                 if (v >= MAXV) break;
                 const int64_t ri = (v < c.nv) ? (int64_t)c.vid[v] * (L - 1) + (k - 1) : zrec;
-                const double2* r = reinterpret_cast<const double2*>(pr + ri * 12);
+                const double2* r = reinterpret_cast<const double2*>(pr + ri * kPairRec);
 #pragma unroll
-                for (int q = 0; q < 6; ++q) a[j][q] = r[q];
+                for (int q = 0; q < kPairRec / 2; ++q) a[j][q] = r[q];
             }
 #pragma unroll
             for (int j = 0; j < GR; ++j) {
                 const int v = v0 + j;
                 if (v >= MAXV) break;
                 const double wv = w[v];
-                S.z0 += wv * a[j][0].x; S.zm += wv * a[j][0].y; S.zk += wv * a[j][1].x;
-                S.wm += wv * a[j][1].y; S.wk += wv * a[j][2].x;
-                S.um0 += wv * a[j][2].y; S.um1 += wv * a[j][3].x; S.um2 += wv * a[j][3].y;
-                S.uk0 += wv * a[j][4].x; S.uk1 += wv * a[j][4].y; S.uk2 += wv * a[j][5].x;
+                S.zm += wv * a[j][0].x; S.zk += wv * a[j][0].y;
+                S.wm += wv * a[j][1].x; S.wk += wv * a[j][1].y;
+                S.um0 += wv * a[j][2].x; S.um1 += wv * a[j][2].y; S.um2 += wv * a[j][3].x;
+                S.uk0 += wv * a[j][3].y; S.uk1 += wv * a[j][4].x; S.uk2 += wv * a[j][4].y;
             }
         }
     }
@@ -656,10 +657,14 @@ __device__ __forceinline__ void pair_sums(const Cell<MAXV>& c, const double* w, 
 
 // Layer + values for one field.  Fast path (monotone cell, finite weights,
 // valid hint h): ONE record per vertex decides whether the layer is h --
-// surface test on z_0, then Q(h), !Q(h-1), !P(h+1) (notation of
-// bracket_scan), i.e. a = b = h, which both the binary search (streamline)
-// and the linear scan (pathline) resolve to h.  Otherwise the exact general
-// bracket runs and the record of the final layer is read.
+// Q(h), !Q(h-1), !P(h+1) (notation of bracket_scan), i.e. a = b = h, which
+// both the binary search (streamline) and the linear scan (pathline) resolve
+// to h -- plus the reference's "above the surface" test d > z_0 + eps first.
+// That test needs no z_0 in the record: for h == 1, z_0 = z_{h-1}; for h >= 2
+// the accepted case has d < z_{h-1} - eps, and in a monotone cell z_{h-1} <=
+// z_1 < z_0 - 1e-6 (margin >> the 1e-9 rounding of the sums), so d > z_0 +
+// eps is false there.  Otherwise the exact general bracket runs and the
+// record of the final layer is read.
 template <int MAXV, bool PATH, int GR>
 __device__ __forceinline__ int layer_eval(const Cell<MAXV>& c, const double* w, bool mono_ok, const Field& f, int L,
                                           double d, int& hint, Pair& S) {
@@ -668,8 +673,8 @@ __device__ __forceinline__ int layer_eval(const Cell<MAXV>& c, const double* w, 
     if (mono_ok && h >= 1 && h <= L - 1) {
         pair_sums<MAXV, GR>(c, w, f.pr, L, h, S);
         bool ok;
-        if (d > S.z0 + eps) {
-            ok = (h == 1);
+        if (h == 1 && d > S.zm + eps) {  // above the surface (z_0 = z_{h-1} here)
+            ok = true;
         } else {
             const bool Qh = d >= S.zk - eps;
             const bool Qm = (h > 1) && (d >= S.zm - eps);
@@ -1275,16 +1280,15 @@ __global__ void pair_record_kernel(int64_t V, int L, const double* zt, const dou
     if (idx >= V * (L - 1)) return;
     const int64_t v = idx / (L - 1);
     const int k = (int)(idx % (L - 1)) + 1;
-    double2* o = reinterpret_cast<double2*>(pr + idx * 12);
+    double2* o = reinterpret_cast<double2*>(pr + idx * kPairRec);
     const double* z = zt + v * L;
     const double* ww = w + v * (L + 1);
     const double* u = vel + (v * L + k - 1) * 3;
-    o[0] = make_double2(z[0], z[k - 1]);
-    o[1] = make_double2(z[k], ww[k - 1]);
-    o[2] = make_double2(ww[k], u[0]);
-    o[3] = make_double2(u[1], u[2]);
-    o[4] = make_double2(u[3], u[4]);
-    o[5] = make_double2(u[5], 0.0);
+    o[0] = make_double2(z[k - 1], z[k]);
+    o[1] = make_double2(ww[k - 1], ww[k]);
+    o[2] = make_double2(u[0], u[1]);
+    o[3] = make_double2(u[2], u[3]);
+    o[4] = make_double2(u[4], u[5]);
 }
 
 __device__ __forceinline__ uint64_t spread3(uint64_t v) {  // 21 bits -> every third bit
@@ -1553,8 +1557,8 @@ int64_t mops_mesh_bytes(const mops_mesh* mesh) { return mesh ? mesh->bytes : 0; 
 static mops_status compute_mono(const mops_mesh* mesh, mops_field* f, hipStream_t s) {
     const int64_t npr = mesh->V * (int64_t)std::max(mesh->L - 1, 0);
     // + one all-zero record at index npr: pair_sums reads it for v >= nv
-    if (!f->d_pr) MOPS_TRY(dmalloc(&f->d_pr, (size_t)((npr + 1) * 12), &f->bytes));
-    HIP_TRY(hipMemsetAsync(f->d_pr + npr * 12, 0, 12 * sizeof(double), s));
+    if (!f->d_pr) MOPS_TRY(dmalloc(&f->d_pr, (size_t)((npr + 1) * kPairRec), &f->bytes));
+    HIP_TRY(hipMemsetAsync(f->d_pr + npr * kPairRec, 0, kPairRec * sizeof(double), s));
     if (npr > 0)
         pair_record_kernel<<<grid_for(npr), kBlock, 0, s>>>(mesh->V, mesh->L, f->d_zt, f->d_vel, f->d_w, f->d_pr);
     if (!f->d_mono) MOPS_TRY(dmalloc(&f->d_mono, (size_t)mesh->C, &f->bytes));
