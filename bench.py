@@ -268,6 +268,12 @@ def main():
         back_snap = synth.make_snapshot(mesh, timestep=1, phase=0.35) if pathline else None
         cpu = cpu_baseline(mesh, snap, back_snap, seeds, seed_cells, args, n_steps)
 
+    if os.environ.get("MOPS_PROF_SECTIONS") == "1":  # experiment builds (-DMOPS_PROF) only
+        import ctypes
+        from mops_amd import _lib
+        buf = (ctypes.c_uint64 * 8)()
+        _lib.load().mops_debug_prof(buf)
+        print("prof counters lane-steps, lane walks, lane loads, wave-steps, wave-steps walking, wave-steps loading:", list(buf), file=sys.stderr)
     if rank == 0:
         line = {
             "metric": "particle-steps/sec",

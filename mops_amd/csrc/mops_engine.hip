@@ -116,8 +116,21 @@ struct mops_field {
 // ===========================================================================
 namespace dev {
 
+// Ablation hooks for perf experiments only (tools/build_variant.sh -DMOPS_ABL_*):
+// they break parity and are never set in a product build.
+#if defined(MOPS_ABL_SQRT)
+__device__ __forceinline__ double xsqrt(double x) { return x * __builtin_amdgcn_rsq(x); }
+#else
+__device__ __forceinline__ double xsqrt(double x) { return sqrt(x); }
+#endif
+#if defined(MOPS_ABL_DIV)
+__device__ __forceinline__ double xdiv(double a, double b) { return a * __builtin_amdgcn_rcp(b); }
+#else
+__device__ __forceinline__ double xdiv(double a, double b) { return a / b; }
+#endif
+
 __device__ __forceinline__ double sq3(double x, double y, double z) { return x * x + y * y + z * z; }
-__device__ __forceinline__ double len3(double x, double y, double z) { return sqrt(sq3(x, y, z)); }
+__device__ __forceinline__ double len3(double x, double y, double z) { return xsqrt(sq3(x, y, z)); }
 
 // The reference's `length(v) < 1e-12` tests (MPASOVisualizerKernels.cpp:841-852)
 // without the square root: correctly rounded sqrt is monotone, and the
@@ -134,16 +147,20 @@ __device__ __forceinline__ double tri_area(double ax, double ay, double az, doub
     const double px = e1y * e2z - e1z * e2y;
     const double py = e1z * e2x - e1x * e2z;
     const double pz = e1x * e2y - e1y * e2x;
-    return sqrt(px * px + py * py + pz * pz) / 2.0;
+    return xsqrt(px * px + py * py + pz * pz) / 2.0;
 }
 
 // TBBKernel::CalcPositionAfterRotation (TBBKernel.h:177-206)
 __device__ __forceinline__ void rotate(double px, double py, double pz, double ax, double ay, double az, double th,
                                        double& rx, double& ry, double& rz) {
+#if defined(MOPS_ABL_TRIG)
+    const double c = 1.0 - 0.5 * th * th, s = th;
+#else
     const double c = cos(th), s = sin(th);
+#endif
     const double al = len3(ax, ay, az);
     if (al <= 1e-12) { rx = px; ry = py; rz = pz; return; }
-    const double ux = ax / al, uy = ay / al, uz = az / al;
+    const double ux = xdiv(ax, al), uy = xdiv(ay, al), uz = xdiv(az, al);
     rx = (c + ux * ux * (1.0 - c)) * px + (ux * uy * (1.0 - c) - uz * s) * py + (ux * uz * (1.0 - c) + uy * s) * pz;
     ry = (uy * ux * (1.0 - c) + uz * s) * px + (c + uy * uy * (1.0 - c)) * py + (uy * uz * (1.0 - c) - ux * s) * pz;
     rz = (uz * ux * (1.0 - c) - uy * s) * px + (uz * uy * (1.0 - c) + ux * s) * py + (c + uz * uz * (1.0 - c)) * pz;
@@ -311,13 +328,13 @@ __device__ __forceinline__ bool weights(const Cell<MAXV>& c, int L, int V, doubl
             const double ny = wrap ? Y[0] : Y[(i + 1) % MAXV];
             const double nz = wrap ? Z[0] : Z[(i + 1) % MAXV];
             Anext = tri_area(X[i], Y[i], Z[i], nx, ny, nz, px, py, pz);
-            w[i] = BB[i] / (Ai * Anext);
+            w[i] = xdiv(BB[i], (Ai * Anext));
             sum += w[i];
         } else {
             w[i] = 0.0;
         }
     }
-    const double recp = 1.0 / sum;
+    const double recp = xdiv(1.0, sum);
 #pragma unroll
     for (int i = 0; i < MAXV; ++i)
         if (i < nv) w[i] *= recp;
@@ -531,6 +548,13 @@ __device__ __forceinline__ int bracket_mono(const Cell<MAXV>& c, const double* w
 // sets the anchor to the cell centre with rs = (min_nb |c_nb - c|)/2 - 1 m,
 // the same argument at p0 = c.  A walk that changes cell leaves the anchor of
 // the new cell's load_cell.
+#if defined(MOPS_PROF)
+// Event counters for perf experiments (tools/build_variant.sh -DMOPS_PROF), read back with
+// mops_debug_prof: [0] lane-steps, [1] lane walks, [2] lane cell loads, [3] wave-steps,
+// [4] wave-steps with a walk, [5] wave-steps with a cell load.  Never set in a product build.
+__device__ unsigned long long g_prof[8];
+#endif
+
 template <int MAXV>
 __device__ __forceinline__ int walk(Cell<MAXV>& c, int cell, double x, double y, double z,
                                     const int* __restrict__ cellrec, const double4* __restrict__ cxyz, int C) {
@@ -636,7 +660,11 @@ __device__ __forceinline__ void pair_sums(const Cell<MAXV>& c, const double* w, 
             for (int j = 0; j < GR; ++j) {
                 const int v = v0 + j;
                 if (v >= MAXV) break;
-                const int64_t ri = (v < c.nv) ? (int64_t)c.vid[v] * (L - 1) + (k - 1) : zrec;
+    #if defined(MOPS_ABL_PAIR1)
+            const int64_t ri = (int64_t)c.vid[0] * (L - 1) + (k - 1);
+#else
+            const int64_t ri = (v < c.nv) ? (int64_t)c.vid[v] * (L - 1) + (k - 1) : zrec;
+#endif
                 const double2* r = reinterpret_cast<const double2*>(pr + ri * kPairRec);
 #pragma unroll
                 for (int q = 0; q < kPairRec / 2; ++q) a[j][q] = r[q];
@@ -808,9 +836,12 @@ struct TrajArgs {
 #ifndef MOPS_GR_R
 #define MOPS_GR_R 2  // RK4
 #endif
-template <bool EULER>
+#ifndef MOPS_GR_PE
+#define MOPS_GR_PE MOPS_GR_E  // pathline Euler
+#endif
+template <bool PATH, bool EULER>
 struct PairGroup {
-    static constexpr int value = EULER ? MOPS_GR_E : MOPS_GR_R;
+    static constexpr int value = EULER ? (PATH ? MOPS_GR_PE : MOPS_GR_E) : MOPS_GR_R;
 };
 // Wide stencils (maxEdges > 7: MAXV 12 / 20) never cache the polygon in
 // registers and ask for fewer waves -- their per-vertex arrays alone would
@@ -861,10 +892,31 @@ __global__ void __launch_bounds__(kTrajBlock, (TrajWaves<MAXV, PATH, EULER>::val
             // neighbour is strictly farther than c by more than rounding, so
             // the reference's argmin (c listed last, strict <) keeps c (dev::walk).
             const double ex = x - c.cx, ey = y - c.cy, ez = z - c.cz;
+#if defined(MOPS_PROF)
+            const bool walking = !(ex * ex + ey * ey + ez * ez < c.rs2);
+            bool loading = false;
+            if (walking) {
+                cell = dev::walk<MAXV>(c, cell, x, y, z, a.cellrec, a.cxyz, C);
+                loading = c.id != cell;
+                if (c.id != cell) dev::load_cell<MAXV, RCache<MAXV, PATH, EULER>::value>(c, cell, a.cellrec, a.vxyz, a.mono0, a.mono1, a.cxyz, a.cellB);
+            }
+            {
+                const unsigned long long bw = __ballot(walking), bl = __ballot(loading), ba = __ballot(1);
+                if ((int)__lane_id() == __builtin_ffsll((long long)ba) - 1) {
+                    atomicAdd(&dev::g_prof[0], (unsigned long long)__popcll(ba));
+                    atomicAdd(&dev::g_prof[1], (unsigned long long)__popcll(bw));
+                    atomicAdd(&dev::g_prof[2], (unsigned long long)__popcll(bl));
+                    atomicAdd(&dev::g_prof[3], 1ull);
+                    atomicAdd(&dev::g_prof[4], bw ? 1ull : 0ull);
+                    atomicAdd(&dev::g_prof[5], bl ? 1ull : 0ull);
+                }
+            }
+#else
             if (!(ex * ex + ey * ey + ez * ez < c.rs2)) {
                 cell = dev::walk<MAXV>(c, cell, x, y, z, a.cellrec, a.cxyz, C);
                 if (c.id != cell) dev::load_cell<MAXV, RCache<MAXV, PATH, EULER>::value>(c, cell, a.cellrec, a.vxyz, a.mono0, a.mono1, a.cxyz, a.cellB);
             }
+#endif
         }
         const double d = -1.0 * (double)dep;
         const double r = dev::len3(x, y, z);
@@ -872,8 +924,8 @@ __global__ void __launch_bounds__(kTrajBlock, (TrajWaves<MAXV, PATH, EULER>::val
         double nx, ny, nz;
         const double alpha = PATH ? (double)step / (double)a.n_steps : 0.0;
         if (EULER) {
-            bool ok = PATH ? dev::eval_path<MAXV, PairGroup<EULER>::value>(c, a.L, a.V, a.f0, a.f1, x, y, z, d, alpha, hint0, hint1, hx, hy, hz, wv)
-                           : dev::eval_stream<MAXV, PairGroup<EULER>::value>(c, a.L, a.V, a.f0, x, y, z, d, hint0, hx, hy, hz, wv);
+            bool ok = PATH ? dev::eval_path<MAXV, PairGroup<PATH, EULER>::value>(c, a.L, a.V, a.f0, a.f1, x, y, z, d, alpha, hint0, hint1, hx, hy, hz, wv)
+                           : dev::eval_stream<MAXV, PairGroup<PATH, EULER>::value>(c, a.L, a.V, a.f0, x, y, z, d, hint0, hx, hy, hz, wv);
             if (!ok) { died = (int)step; break; }
             const double ax = y * hz - z * hy, ay = z * hx - x * hz, az = x * hy - y * hx;
             const double speed = dev::len3(hx, hy, hz);
@@ -884,22 +936,22 @@ __global__ void __launch_bounds__(kTrajBlock, (TrajWaves<MAXV, PATH, EULER>::val
             double s1x, s1y, s1z, s1w, s2x, s2y, s2z, s2w, s3x, s3y, s3z, s3w, s4x, s4y, s4z, s4w;
             double qx, qy, qz;
             const double a1 = alpha;
-            bool ok = PATH ? dev::eval_path<MAXV, PairGroup<EULER>::value>(c, a.L, a.V, a.f0, a.f1, x, y, z, d, a1, hint0, hint1, s1x, s1y, s1z, s1w)
-                           : dev::eval_stream<MAXV, PairGroup<EULER>::value>(c, a.L, a.V, a.f0, x, y, z, d, hint0, s1x, s1y, s1z, s1w);
+            bool ok = PATH ? dev::eval_path<MAXV, PairGroup<PATH, EULER>::value>(c, a.L, a.V, a.f0, a.f1, x, y, z, d, a1, hint0, hint1, s1x, s1y, s1z, s1w)
+                           : dev::eval_stream<MAXV, PairGroup<PATH, EULER>::value>(c, a.L, a.V, a.f0, x, y, z, d, hint0, s1x, s1y, s1z, s1w);
             if (!ok) { died = (int)step; break; }
             dev::advect(x, y, z, s1x, s1y, s1z, dt * 0.5, qx, qy, qz);
             const double a2 = PATH ? dev::dclamp(a1 + 0.5 * a.dalpha, 0.0, 1.0) : 0.0;
-            ok = PATH ? dev::eval_path<MAXV, PairGroup<EULER>::value>(c, a.L, a.V, a.f0, a.f1, qx, qy, qz, d, a2, hint0, hint1, s2x, s2y, s2z, s2w)
-                      : dev::eval_stream<MAXV, PairGroup<EULER>::value>(c, a.L, a.V, a.f0, qx, qy, qz, d, hint0, s2x, s2y, s2z, s2w);
+            ok = PATH ? dev::eval_path<MAXV, PairGroup<PATH, EULER>::value>(c, a.L, a.V, a.f0, a.f1, qx, qy, qz, d, a2, hint0, hint1, s2x, s2y, s2z, s2w)
+                      : dev::eval_stream<MAXV, PairGroup<PATH, EULER>::value>(c, a.L, a.V, a.f0, qx, qy, qz, d, hint0, s2x, s2y, s2z, s2w);
             if (!ok) { died = (int)step; break; }
             dev::advect(x, y, z, s2x, s2y, s2z, dt * 0.5, qx, qy, qz);
-            ok = PATH ? dev::eval_path<MAXV, PairGroup<EULER>::value>(c, a.L, a.V, a.f0, a.f1, qx, qy, qz, d, a2, hint0, hint1, s3x, s3y, s3z, s3w)
-                      : dev::eval_stream<MAXV, PairGroup<EULER>::value>(c, a.L, a.V, a.f0, qx, qy, qz, d, hint0, s3x, s3y, s3z, s3w);
+            ok = PATH ? dev::eval_path<MAXV, PairGroup<PATH, EULER>::value>(c, a.L, a.V, a.f0, a.f1, qx, qy, qz, d, a2, hint0, hint1, s3x, s3y, s3z, s3w)
+                      : dev::eval_stream<MAXV, PairGroup<PATH, EULER>::value>(c, a.L, a.V, a.f0, qx, qy, qz, d, hint0, s3x, s3y, s3z, s3w);
             if (!ok) { died = (int)step; break; }
             dev::advect(x, y, z, s3x, s3y, s3z, dt, qx, qy, qz);
             const double a4 = PATH ? dev::dclamp(a1 + a.dalpha, 0.0, 1.0) : 0.0;
-            ok = PATH ? dev::eval_path<MAXV, PairGroup<EULER>::value>(c, a.L, a.V, a.f0, a.f1, qx, qy, qz, d, a4, hint0, hint1, s4x, s4y, s4z, s4w)
-                      : dev::eval_stream<MAXV, PairGroup<EULER>::value>(c, a.L, a.V, a.f0, qx, qy, qz, d, hint0, s4x, s4y, s4z, s4w);
+            ok = PATH ? dev::eval_path<MAXV, PairGroup<PATH, EULER>::value>(c, a.L, a.V, a.f0, a.f1, qx, qy, qz, d, a4, hint0, hint1, s4x, s4y, s4z, s4w)
+                      : dev::eval_stream<MAXV, PairGroup<PATH, EULER>::value>(c, a.L, a.V, a.f0, qx, qy, qz, d, hint0, s4x, s4y, s4z, s4w);
             if (!ok) { died = (int)step; break; }
             // (s1 + 2 s2 + 2 s3 + s4) / 6 -- cy::Vec3 operator order (:959-960)
             hx = (((s1x + s2x * 2.0) + s3x * 2.0) + s4x) / 6.0;
@@ -918,7 +970,7 @@ __global__ void __launch_bounds__(kTrajBlock, (TrajWaves<MAXV, PATH, EULER>::val
         const double r_new = dev::dmax(1.0, r + wv * (double)a.delta_t);
         dep = (float)nd;
         const double nl = dev::len3(nx, ny, nz);
-        if (nl > 1e-12) { nx = (nx / nl) * r_new; ny = (ny / nl) * r_new; nz = (nz / nl) * r_new; }
+        if (nl > 1e-12) { nx = dev::xdiv(nx, nl) * r_new; ny = dev::xdiv(ny, nl) * r_new; nz = dev::xdiv(nz, nl) * r_new; }
         if (step == 0) {  // first_vel (:988-991)
             a.rec[3 * a.rec_stride + pid] = hx;
             a.rec[4 * a.rec_stride + pid] = hy;
@@ -1405,6 +1457,18 @@ void launch_traj(const TrajArgs& a, bool path, bool euler, hipStream_t s) {
 extern "C" {
 
 const char* mops_last_error(void) { return g_last_error.c_str(); }
+#if defined(MOPS_PROF)
+// experiment builds only: read and clear the event counters (dev::g_prof)
+int mops_debug_prof(uint64_t* out) {
+    unsigned long long h[8];
+    if (hipDeviceSynchronize() != hipSuccess) return -1;
+    if (hipMemcpyFromSymbol(h, HIP_SYMBOL(dev::g_prof), sizeof(h)) != hipSuccess) return -1;
+    for (int i = 0; i < 8; ++i) out[i] = h[i];
+    const unsigned long long z[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    if (hipMemcpyToSymbol(HIP_SYMBOL(dev::g_prof), z, sizeof(z)) != hipSuccess) return -1;
+    return 0;
+}
+#endif
 int32_t mops_abi_version(void) { return MOPS_ABI_VERSION; }
 
 mops_status mops_mesh_create(const mops_mesh_desc* desc, void* stream, mops_mesh** out) {
@@ -1828,8 +1892,12 @@ mops_status mops_traj_advance(const mops_mesh* mesh, const mops_field* front, co
     hipStream_t s = (hipStream_t)stream;
     switch (mesh->maxv) {
         case 7: launch_traj<7>(a, back != nullptr, euler, s); break;
+#if !defined(MOPS_ONLY7)  // experiment builds: MAXV 7 instantiations only
         case 12: launch_traj<12>(a, back != nullptr, euler, s); break;
         default: launch_traj<20>(a, back != nullptr, euler, s); break;
+#else
+        default: return fail(MOPS_ERR_UNSUPPORTED, "experiment build: MAXV 7 only");
+#endif
     }
     HIP_TRY(hipGetLastError());
     return MOPS_OK;

@@ -1,0 +1,130 @@
+"""Parity at BASELINE.json's full sizes: the config-2 and
+config-3 workloads on the EC30to60-class mesh (235 567 cells, 60 levels).
+
+The oracle cannot run 1e6-1e7 particles for a day in seconds, so the full-size
+checks are
+  * a random sample of the SAME device run (particles are independent: every
+    sampled line must equal the oracle's line for that seed, bit for bit,
+    whatever the other particles did), dead particles over-sampled;
+  * size-independent properties of the whole run: sharding the particle set
+    (the multi-GPU partition, §8e) reproduces the unsharded records bit for bit,
+    and every line of a live particle is finite and on its shell.
+"""
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def ec_case(gpu, engine_lib, oracle_lib):
+    from mops_amd import synth
+    from mops_amd.engine import DeviceField, DeviceMesh
+    mesh = synth.make_mesh(158, n_levels=60)
+    s0 = synth.make_snapshot(mesh, timestep=0)
+    s1 = synth.make_snapshot(mesh, timestep=1, phase=0.35)
+    dm = DeviceMesh.from_mesh(mesh)
+    f0, f1 = DeviceField.from_snapshot(dm, s0), DeviceField.from_snapshot(dm, s1)
+    r0, r1 = oracle_lib.preprocess(mesh, s0), oracle_lib.preprocess(mesh, s1)
+    return mesh, dm, f0, f1, r0, r1
+
+
+def _run_device(dm, f0, f1, cfg, seeds, depth):
+    """Device-resident run (the bench path): returns seed cells, death steps and a
+    lazily-indexable view of the finalized lines (seed order)."""
+    import torch
+    from mops_amd.engine import ParticleSet
+    ps = ParticleSet(dm, seeds, depth, cfg)
+    cells = ps.original(ps.cell).cpu().numpy()
+    ps.advance(f0, f1, 0, cfg.n_steps)
+    lines = ps.finalize(pathline=f1 is not None)
+    death = ps.original(ps.death).cpu().numpy()
+    torch.cuda.synchronize()
+    return ps, cells, death, lines
+
+
+def _sample(n, death, k=384, k_dead=64, seed=0):
+    rng = np.random.default_rng(seed)
+    dead = np.flatnonzero(death >= 0)
+    idx = rng.choice(n, k, replace=False)
+    if dead.size:
+        idx = np.concatenate([idx, rng.choice(dead, min(k_dead, dead.size), replace=False)])
+    return np.unique(idx)
+
+
+def _check_sample(lines, death, idx, ref, pathline):
+    import torch
+    ti = torch.as_tensor(idx, device=lines["points"].device)
+    pts = lines["points"][ti].cpu().numpy()
+    vel = lines["velocity"][ti].cpu().numpy()
+    assert np.array_equal(death[idx], ref["death"]), "death steps differ from the oracle"
+    assert np.array_equal(pts, ref["points"]), "sampled lines differ from the oracle"
+    assert np.array_equal(vel, ref["velocity"]), "sampled velocities differ from the oracle"
+    assert np.array_equal(lines["lastPoint"][ti].cpu().numpy(), ref["lastPoint"])
+    if pathline:
+        assert np.array_equal(lines["temperature"][ti].cpu().numpy(), ref["temperature"])
+
+
+def _check_shells(lines, death):
+    """Every point of a particle that never died is finite and within 1 km of
+    the sphere it started on (w*dt moves r by millimetres per step)."""
+    import torch
+    live = torch.as_tensor(death < 0, device=lines["points"].device)
+    p = lines["points"][live]
+    assert torch.isfinite(p).all()
+    r = torch.linalg.norm(p, dim=-1)
+    assert (r - r[:, :1]).abs().max().item() < 1e3
+
+
+def test_config2_full_size(ec_case, oracle_lib):
+    """BASELINE config 2: 1e6 particles, depth 800 m, dt 120 s, 1-day Euler streamline."""
+    import torch
+    import bench
+    from mops_amd.engine import TrajectoryConfig
+    mesh, dm, f0, _, r0, _ = ec_case
+    seeds = bench.make_seeds(1_000_000, 0)
+    cfg = TrajectoryConfig(deltaT=120, simulationDuration=86400, recordT=3600, depth=800.0, method=1)
+    ps, cells, death, lines = _run_device(dm, f0, None, cfg, seeds, 800.0)
+    idx = _sample(len(seeds), death)
+    ref = oracle_lib.run(mesh, r0, None, seeds[idx], depth=800.0, delta_t=120, duration=86400, record_t=3600,
+                         euler=True, cells=cells[idx])
+    _check_sample(lines, death, idx, ref, pathline=False)
+    _check_shells(lines, death)
+    # the multi-GPU partition (contiguous shards, §8e) reproduces the unsharded run bit for bit
+    half = len(seeds) // 2
+    for lo, hi in ((0, half), (half, len(seeds))):
+        _, _, d_s, l_s = _run_device(dm, f0, None, cfg, seeds[lo:hi], 800.0)
+        assert np.array_equal(d_s, death[lo:hi])
+        assert torch.equal(l_s["points"], lines["points"][lo:hi])
+        assert torch.equal(l_s["velocity"], lines["velocity"][lo:hi])
+
+
+def test_config2_full_size_rk4(ec_case, oracle_lib):
+    """Config-2 shape with RK4 (Q1 cell-crossing deaths at full resolution)."""
+    import bench
+    from mops_amd.engine import TrajectoryConfig
+    mesh, dm, f0, _, r0, _ = ec_case
+    seeds = bench.make_seeds(1_000_000, 0)
+    cfg = TrajectoryConfig(deltaT=120, simulationDuration=86400, recordT=3600, depth=800.0, method=0)
+    _, cells, death, lines = _run_device(dm, f0, None, cfg, seeds, 800.0)
+    assert (death >= 0).any()  # Q1 is exercised at this resolution
+    idx = _sample(len(seeds), death, seed=1)
+    ref = oracle_lib.run(mesh, r0, None, seeds[idx], depth=800.0, delta_t=120, duration=86400, record_t=3600,
+                         euler=False, cells=cells[idx])
+    _check_sample(lines, death, idx, ref, pathline=False)
+
+
+def test_config3_full_size_pair(ec_case, oracle_lib):
+    """BASELINE config 3, one daily pair: 1e7 particles at layer 10, dt 60 s, Euler pathline."""
+    import bench
+    from mops_amd.engine import TrajectoryConfig
+    mesh, dm, f0, f1, r0, r1 = ec_case
+    depth = bench.layer_mid_depth(mesh, 10)
+    seeds = bench.make_seeds(10_000_000, 0)
+    cfg = TrajectoryConfig(deltaT=60, simulationDuration=86400, recordT=3600, depth=depth, method=1)
+    _, cells, death, lines = _run_device(dm, f0, f1, cfg, seeds, depth)
+    idx = _sample(len(seeds), death, k=256, seed=2)
+    ref = oracle_lib.run(mesh, r0, r1, seeds[idx], depth=depth, delta_t=60, duration=86400, record_t=3600,
+                         euler=True, cells=cells[idx])
+    _check_sample(lines, death, idx, ref, pathline=True)
+    _check_shells(lines, death)
