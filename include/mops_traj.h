@@ -155,6 +155,16 @@ int64_t mops_field_bytes(const mops_field* field);
 mops_status mops_locate_cells(const mops_mesh* mesh, int64_t n, const double* d_points, int32_t* d_cells,
                               void* stream);
 
+/* Same answer as mops_locate_cells, faster when a candidate cell per point is
+ * known (d_hint [n], device, may be NULL; entries outside [0, C) are
+ * ignored): a point within half the distance from its hint's centre to the
+ * nearest OTHER centre (less 1 m) provably has the hint as its unique nearest
+ * centre, and skips the search.  Used between chained pathline pairs, where
+ * each continuation point's hint is the cell its particle ended in
+ * (pyMOPSAPI.py:1446-1459 re-locates every pair's seeds). */
+mops_status mops_locate_cells_hinted(const mops_mesh* mesh, int64_t n, const double* d_points,
+                                     const int32_t* d_hint, int32_t* d_cells, void* stream);
+
 /* Locality order for n particles: sorts particle indices by a Morton key
  * of their current cell centre, so a wavefront's lanes share cell stencils
  * (no reference counterpart: the reference processes particles in index

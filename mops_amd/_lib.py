@@ -18,7 +18,7 @@ EXPORTED = (
     "mops_mesh_create", "mops_mesh_destroy", "mops_mesh_bytes",
     "mops_field_create", "mops_field_create_device", "mops_field_rebuild_device", "mops_field_create_derived", "mops_field_export", "mops_cell_to_vertex_attr",
     "mops_field_destroy", "mops_field_bytes",
-    "mops_locate_cells", "mops_order_particles",
+    "mops_locate_cells", "mops_locate_cells_hinted", "mops_order_particles",
     "mops_traj_num_records", "mops_traj_num_steps", "mops_traj_advance", "mops_traj_finalize",
     "mops_remove_nan_lines", "mops_run_trajectories",
     # include/mops_io.h
@@ -111,6 +111,7 @@ def load(path: str | None = None):
     lib.mops_field_destroy.argtypes = [P]; lib.mops_field_destroy.restype = None
     lib.mops_field_bytes.argtypes = [P]; lib.mops_field_bytes.restype = I64
     lib.mops_locate_cells.argtypes = [P, I64, P, P, P]; lib.mops_locate_cells.restype = st
+    lib.mops_locate_cells_hinted.argtypes = [P, I64, P, P, P, P]; lib.mops_locate_cells_hinted.restype = st
     lib.mops_order_particles.argtypes = [P, I64, P, P, P]; lib.mops_order_particles.restype = st
     lib.mops_traj_num_records.argtypes = [P]; lib.mops_traj_num_records.restype = I64
     lib.mops_traj_num_steps.argtypes = [P]; lib.mops_traj_num_steps.restype = I64

@@ -106,7 +106,8 @@ class PathlineChain:
                     d = pdep
                 else:
                     d = cfg.depth
-                ps.reseed(s, d, stream=cs.cuda_stream)
+                # a continuation pair: each particle's current cell is an exact-locate hint
+                ps.reseed(s, d, stream=cs.cuda_stream, hint_cells=(p > 0 and follow_last))
                 front, back = fields[p], fields[p + 1]
                 for s0 in range(0, cfg.n_steps, period):
                     if timing is not None:

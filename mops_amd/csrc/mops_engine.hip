@@ -85,6 +85,7 @@ struct mops_mesh {
     int* d_bcells = nullptr;      // cell ids in key order [C]
     uint64_t* d_cell_key = nullptr;  // Morton key of each cell centre (particle locality order)
     double* d_cellB = nullptr;       // [C][maxv] Wachspress B_i of each cell polygon
+    double* d_rloc2 = nullptr;       // [C] squared hinted-locate radius (locate_radius_kernel)
     // grow-only scratch for mops_order_particles (not re-entrant, like the reference's global app)
     mutable void* d_scratch = nullptr;
     mutable size_t scratch_bytes = 0;
@@ -99,6 +100,7 @@ struct mops_field {
     double* d_vel = nullptr;  // cellVertexVelocity [V][L][3]
     double* d_w = nullptr;    // cellVertexVertVelocity [V][L+1]
     uint8_t* d_mono = nullptr;  // [C] 1 = every vertex column of the cell strictly decreasing (margin)
+    uint8_t* d_vmono = nullptr;  // [V] the same test per vertex column (mono_kernel's first pass)
     // level-pair records [V][L-1][kPairRec] doubles, record k-1 of vertex v =
     // {z_{k-1}, z_k, w_{k-1}, w_k, vel_{k-1} (3), vel_k (3)}: one 80-B,
     // 16-B-aligned read (5 x dwordx4) gives a vertex's whole contribution when
@@ -1216,7 +1218,8 @@ __device__ __forceinline__ int64_t lower_bound_u64(const uint64_t* a, int64_t n,
 }
 
 __device__ __forceinline__ void consider(const double4* cxyz, int cid, double qx, double qy, double qz, double& best,
-                                         int& bi) {
+                                         int& bi, int exclude) {
+    if (cid == exclude) return;
     const double4 p = cxyz[cid];
     const double d0 = qx - p.x, d1 = qy - p.y, d2 = qz - p.z;
     double dd = 0.0;
@@ -1224,16 +1227,11 @@ __device__ __forceinline__ void consider(const double4* cxyz, int cid, double qx
     if (dd < best || (dd == best && cid < bi)) { best = dd; bi = cid; }
 }
 
-__global__ void locate_kernel(int64_t n, const double* pts, int64_t C, const double4* cxyz, const uint64_t* keys,
-                              const int* ids, double origin, double h, int origin_cell, int* out) {
-    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= n) return;
-    const double qx = pts[3 * i], qy = pts[3 * i + 1], qz = pts[3 * i + 2];
-    // (0,0,0) is where a particle that died before its first record continues
-    // from in a pair chain (lastPoint = 0, quirk Q1); its exact answer is
-    // precomputed instead of scanning every cell
-    if (qx == 0.0 && qy == 0.0 && qz == 0.0) { out[i] = origin_cell; return; }
-    double best = INFINITY;
+// Exact nearest cell centre to q (smallest id on ties), `exclude` skipped: bucket shells
+// around q until the best distance is provably final, else an exhaustive scan.
+__device__ int nearest_centre(double qx, double qy, double qz, int64_t C, const double4* cxyz, const uint64_t* keys,
+                              const int* ids, double origin, double h, int exclude, double& best) {
+    best = INFINITY;
     int bi = -1;
     const int kMaxShell = 6;
     const int64_t kLim = (int64_t)1 << 21;
@@ -1251,17 +1249,65 @@ __global__ void locate_kernel(int64_t n, const double* pts, int64_t C, const dou
                         if (ix < 0 || iy < 0 || iz < 0 || ix >= kLim || iy >= kLim || iz >= kLim) continue;
                         const uint64_t key = bkey(ix, iy, iz);
                         int64_t j = lower_bound_u64(keys, C, key);
-                        for (; j < C && keys[j] == key; ++j) consider(cxyz, ids[j], qx, qy, qz, best, bi);
+                        for (; j < C && keys[j] == key; ++j) consider(cxyz, ids[j], qx, qy, qz, best, bi, exclude);
                     }
             // every point outside shells 0..s is at least s*h away
             const double bound = (double)s * h;
             if (bi >= 0 && best <= bound * bound) done = true;
         }
         if (!done) {  // far from every cell centre: exhaustive scan
-            for (int64_t cid = 0; cid < C; ++cid) consider(cxyz, (int)cid, qx, qy, qz, best, bi);
+            for (int64_t cid = 0; cid < C; ++cid) consider(cxyz, (int)cid, qx, qy, qz, best, bi, exclude);
         }
     }
-    out[i] = bi;
+    return bi;
+}
+
+// MPASOField::calcInWhichCells (MPASOField.cpp:23-34): exact 1-NN over the cell centres.
+// With `hint` (a candidate cell per point, e.g. the cell a chained particle ended the
+// previous pair in): if q lies within rloc(h) = d_nn(h)/2 - 1 m of centre h, where d_nn(h)
+// is the distance from h to the nearest OTHER centre, then every other centre c' has
+// |q - c'| >= d_nn - |q - h| > |q - h| + 2 m, so h is the unique exact answer and the
+// search is skipped.  Any hint (or none) gives the same result.
+__global__ void locate_kernel(int64_t n, const double* pts, int64_t C, const double4* cxyz, const uint64_t* keys,
+                              const int* ids, double origin, double h, int origin_cell, const int* hint,
+                              const double* rloc2, int* out) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const double qx = pts[3 * i], qy = pts[3 * i + 1], qz = pts[3 * i + 2];
+    // (0,0,0) is where a particle that died before its first record continues
+    // from in a pair chain (lastPoint = 0, quirk Q1); its exact answer is
+    // precomputed instead of scanning every cell
+    if (qx == 0.0 && qy == 0.0 && qz == 0.0) { out[i] = origin_cell; return; }
+    if (hint) {
+        const int hc = hint[i];
+        if (hc >= 0 && hc < C) {
+            const double4 p = cxyz[hc];
+            const double d0 = qx - p.x, d1 = qy - p.y, d2 = qz - p.z;
+            if (d0 * d0 + d1 * d1 + d2 * d2 < rloc2[hc]) { out[i] = hc; return; }
+        }
+    }
+    double best;
+    out[i] = nearest_centre(qx, qy, qz, C, cxyz, keys, ids, origin, h, -1, best);
+}
+
+// rloc(c)^2 for the hinted locate: half the distance to the nearest other centre, shrunk
+// by 1e-9 relative and 1 m absolute (>> the rounding of |q - c| at Earth radius); -1 when
+// another centre coincides with c (never taken)
+__global__ void locate_radius_kernel(int64_t C, const double4* cxyz, const uint64_t* keys, const int* ids,
+                                     double origin, double h, double* rloc2) {
+    const int64_t c = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (c >= C) return;
+    const double4 p = cxyz[c];
+    double best;
+    const int nb = nearest_centre(p.x, p.y, p.z, C, cxyz, keys, ids, origin, h, (int)c, best);
+    double r2 = -1.0;
+    if (nb < 0) {
+        r2 = INFINITY;  // the only centre: every point's nearest
+    } else if (best > 0.0 && isfinite(best)) {
+        const double r = 0.5 * sqrt(best) * (1.0 - 1e-9) - 1.0;
+        if (r > 0.0) r2 = r * r * (1.0 - 1e-9);
+    }
+    rloc2[c] = r2;
 }
 
 // ===========================================================================
@@ -1269,24 +1315,28 @@ __global__ void locate_kernel(int64_t n, const double* pts, int64_t C, const dou
 // ===========================================================================
 
 // d_mono[c] = 1 iff every vertex column of cell c is finite, |z| <= 1e6 m and
-// strictly decreasing by >= 1e-6 m per level (see bracket_mono).
-__global__ void mono_kernel(int64_t C, int maxv, int rec_ints, const int* cellrec, const double* zt, int L,
+// strictly decreasing by >= 1e-6 m per level (see bracket_mono).  Two passes:
+// a per-vertex flag from one coalesced (vertex, level) element per thread
+// (every level's test reads the raw z_{l-1}, exactly as the per-column scan),
+// then a per-cell AND over the polygon's vertices.
+__global__ void vertex_mono_kernel(int64_t V, int L, const double* __restrict__ zt, uint8_t* __restrict__ vflag) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= V * L) return;
+    const int l = (int)(i % L);
+    const double z = zt[i];
+    bool ok = isfinite(z) && fabs(z) <= 1e6;
+    if (l > 0) ok = ok && (z < zt[i - 1] - 1e-6);
+    if (!ok) vflag[i / L] = 0;  // every writer stores 0: the race is benign
+}
+
+__global__ void mono_kernel(int64_t C, int maxv, int rec_ints, const int* cellrec, const uint8_t* vflag, int L,
                             uint8_t* mono) {
     const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= C) return;
     const int* r = cellrec + i * rec_ints;
     const int nv = r[0];
     bool ok = (nv >= 1 && nv <= kMaxVertex && L >= 2);
-    for (int k = 0; k < nv && ok; ++k) {
-        const double* col = zt + (int64_t)r[1 + k] * L;
-        double prev = col[0];
-        ok = isfinite(prev) && fabs(prev) <= 1e6;
-        for (int l = 1; l < L && ok; ++l) {
-            const double z = col[l];
-            ok = isfinite(z) && fabs(z) <= 1e6 && (z < prev - 1e-6);
-            prev = z;
-        }
-    }
+    for (int k = 0; k < nv && ok; ++k) ok = vflag[r[1 + k]] != 0;
     mono[i] = ok ? 1 : 0;
 }
 
@@ -1422,14 +1472,14 @@ mops_status upload(const T* h, size_t count, T** d, int64_t* acc, hipStream_t s)
 void free_mesh(mops_mesh* m) {
     if (!m) return;
     (void)hipFree(m->d_cellrec); (void)hipFree(m->d_cxyz); (void)hipFree(m->d_vxyz); (void)hipFree(m->d_cov);
-    (void)hipFree(m->d_bkeys); (void)hipFree(m->d_bcells); (void)hipFree(m->d_cell_key); (void)hipFree(m->d_cellB);
+    (void)hipFree(m->d_bkeys); (void)hipFree(m->d_bcells); (void)hipFree(m->d_cell_key); (void)hipFree(m->d_cellB); (void)hipFree(m->d_rloc2);
     (void)hipFree(m->d_scratch);
     delete m;
 }
 
 void free_field(mops_field* f) {
     if (!f) return;
-    (void)hipFree(f->d_zt); (void)hipFree(f->d_vel); (void)hipFree(f->d_w); (void)hipFree(f->d_mono);
+    (void)hipFree(f->d_zt); (void)hipFree(f->d_vel); (void)hipFree(f->d_w); (void)hipFree(f->d_mono); (void)hipFree(f->d_vmono);
     (void)hipFree(f->d_pr);
     (void)hipFree(f->d_ztc); (void)hipFree(f->d_velc);
     delete f;
@@ -1601,6 +1651,9 @@ mops_status mops_mesh_create(const mops_mesh_desc* desc, void* stream, mops_mesh
     if (e != hipSuccess) { free_mesh(m); return fail(MOPS_ERR_HIP, std::string("bucket sort: ") + hipGetErrorString(e)); }
     if ((st = dmalloc(&m->d_cell_key, (size_t)C, &acc)) != MOPS_OK) { free_mesh(m); return st; }
     cell_key_kernel<<<grid_for(C), kBlock, 0, s>>>(C, m->d_cxyz, m->d_cell_key);
+    if ((st = dmalloc(&m->d_rloc2, (size_t)C, &acc)) != MOPS_OK) { free_mesh(m); return st; }
+    locate_radius_kernel<<<grid_for(C), kBlock, 0, s>>>(C, m->d_cxyz, m->d_bkeys, m->d_bcells, m->bucket_origin,
+                                                        m->bucket_h, m->d_rloc2);
     if ((st = dmalloc(&m->d_cellB, (size_t)(C * m->maxv), &acc)) != MOPS_OK) { free_mesh(m); return st; }
     switch (m->maxv) {
         case 7: cell_b_kernel<7><<<grid_for(C), kBlock, 0, s>>>(C, m->d_cellrec, m->d_vxyz, m->d_cellB); break;
@@ -1626,7 +1679,10 @@ static mops_status compute_mono(const mops_mesh* mesh, mops_field* f, hipStream_
     if (npr > 0)
         pair_record_kernel<<<grid_for(npr), kBlock, 0, s>>>(mesh->V, mesh->L, f->d_zt, f->d_vel, f->d_w, f->d_pr);
     if (!f->d_mono) MOPS_TRY(dmalloc(&f->d_mono, (size_t)mesh->C, &f->bytes));
-    mono_kernel<<<grid_for(mesh->C), kBlock, 0, s>>>(mesh->C, mesh->maxv, mesh->rec_ints, mesh->d_cellrec, f->d_zt,
+    if (!f->d_vmono) MOPS_TRY(dmalloc(&f->d_vmono, (size_t)mesh->V, &f->bytes));
+    HIP_TRY(hipMemsetAsync(f->d_vmono, 1, (size_t)mesh->V, s));
+    vertex_mono_kernel<<<grid_for(mesh->V * mesh->L), kBlock, 0, s>>>(mesh->V, mesh->L, f->d_zt, f->d_vmono);
+    mono_kernel<<<grid_for(mesh->C), kBlock, 0, s>>>(mesh->C, mesh->maxv, mesh->rec_ints, mesh->d_cellrec, f->d_vmono,
                                                     mesh->L, f->d_mono);
     HIP_TRY(hipGetLastError());
     return MOPS_OK;
@@ -1803,7 +1859,21 @@ mops_status mops_locate_cells(const mops_mesh* mesh, int64_t n, const double* d_
     if (n == 0) return MOPS_OK;
     hipStream_t s = (hipStream_t)stream;
     locate_kernel<<<grid_for(n), kBlock, 0, s>>>(n, d_points, mesh->C, mesh->d_cxyz, mesh->d_bkeys, mesh->d_bcells,
-                                                 mesh->bucket_origin, mesh->bucket_h, mesh->origin_cell, d_cells);
+                                                 mesh->bucket_origin, mesh->bucket_h, mesh->origin_cell, nullptr,
+                                                 nullptr, d_cells);
+    HIP_TRY(hipGetLastError());
+    return MOPS_OK;
+}
+
+mops_status mops_locate_cells_hinted(const mops_mesh* mesh, int64_t n, const double* d_points, const int32_t* d_hint,
+                                     int32_t* d_cells, void* stream) {
+    if (!mesh || n < 0 || (n > 0 && (!d_points || !d_cells)))
+        return fail(MOPS_ERR_INVALID, "mops_locate_cells_hinted: invalid argument");
+    if (n == 0) return MOPS_OK;
+    hipStream_t s = (hipStream_t)stream;
+    locate_kernel<<<grid_for(n), kBlock, 0, s>>>(n, d_points, mesh->C, mesh->d_cxyz, mesh->d_bkeys, mesh->d_bcells,
+                                                 mesh->bucket_origin, mesh->bucket_h, mesh->origin_cell, d_hint,
+                                                 d_hint ? mesh->d_rloc2 : nullptr, d_cells);
     HIP_TRY(hipGetLastError());
     return MOPS_OK;
 }

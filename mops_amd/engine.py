@@ -90,10 +90,16 @@ class DeviceMesh:
     def nbytes(self) -> int:
         return int(L.load().mops_mesh_bytes(self.handle))
 
-    def locate(self, d_points, d_cells, n: int, stream=None):
-        """Device pointers (ints) -> nearest cell ids (mops_locate_cells)."""
-        L.check(L.load().mops_locate_cells(self.handle, n, C.c_void_p(d_points), C.c_void_p(d_cells),
-                                           _stream_handle(stream)), "mops_locate_cells")
+    def locate(self, d_points, d_cells, n: int, stream=None, d_hint=None):
+        """Device pointers (ints) -> nearest cell ids (mops_locate_cells; with a
+        candidate cell per point, mops_locate_cells_hinted -- same answer)."""
+        if d_hint is None:
+            L.check(L.load().mops_locate_cells(self.handle, n, C.c_void_p(d_points), C.c_void_p(d_cells),
+                                               _stream_handle(stream)), "mops_locate_cells")
+        else:
+            L.check(L.load().mops_locate_cells_hinted(self.handle, n, C.c_void_p(d_points), C.c_void_p(d_hint),
+                                                      C.c_void_p(d_cells), _stream_handle(stream)),
+                    "mops_locate_cells_hinted")
 
     def close(self):
         if getattr(self, "handle", None):
@@ -301,14 +307,19 @@ class ParticleSet:
         self.records.zero_()
         self._written = False
 
-    def reseed(self, seeds, depth, stream=None):
+    def reseed(self, seeds, depth, stream=None, hint_cells: bool = False):
         """Start a new run from device-resident seeds [n,3] (f64) and depth (scalar
         or [n] f32): state <- seeds, death cleared, records zeroed, seed cells
-        located (the reference's calcInWhichCells per run) and re-ordered."""
+        located (the reference's calcInWhichCells per run) and re-ordered.
+        ``hint_cells``: the seeds continue this set's particles (a chained pair),
+        so each particle's current cell seeds the exact locate (same answer)."""
         torch = self.torch
         s = seeds.reshape(-1, 3)
         if int(s.shape[0]) != self.n:
             raise ValueError("reseed: particle count changed")
+        h = stream if stream is not None else torch.cuda.current_stream(self.seeds.device).cuda_stream
+        # slot order -> particle order, before the ids reset (same stream as the copies below)
+        hint = self.original(self.cell) if hint_cells else None
         self.seeds.copy_(s)
         self.ids.copy_(torch.arange(self.n, dtype=torch.int32, device=self.ids.device))
         self.x.copy_(s[:, 0]); self.y.copy_(s[:, 1]); self.z.copy_(s[:, 2])
@@ -319,8 +330,8 @@ class ParticleSet:
         self.death.fill_(-1)
         self.records.zero_()
         self._written = False
-        h = stream if stream is not None else torch.cuda.current_stream(self.seeds.device).cuda_stream
-        self.mesh.locate(self.seeds.data_ptr(), self.cell.data_ptr(), self.n, stream=h)
+        self.mesh.locate(self.seeds.data_ptr(), self.cell.data_ptr(), self.n, stream=h,
+                         d_hint=None if hint is None else hint.data_ptr())
         self.reorder(stream=h)
 
     def particles(self) -> L.Particles:

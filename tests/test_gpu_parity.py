@@ -92,6 +92,16 @@ def test_locate_matches_bruteforce(gpu, dev_small, small_case, oracle_lib):
     dm.locate(d.data_ptr(), out.data_ptr(), len(pts))
     torch.cuda.synchronize()
     assert np.array_equal(out.cpu().numpy(), ref)
+    # hinted locate (chained pairs): the same answer for exact, neighbouring, random and invalid hints
+    rng = np.random.default_rng(4)
+    coc = mesh.cellsOnCell.astype(np.int64).reshape(mesh.nCells, -1) - 1
+    nb = coc[np.clip(ref, 0, None), rng.integers(0, 5, len(ref))]
+    for hint in (ref, nb, rng.integers(0, mesh.nCells, len(ref)), np.full(len(ref), -7)):
+        hd = torch.as_tensor(np.ascontiguousarray(hint, dtype=np.int32), device=gpu)
+        out.fill_(-99)
+        dm.locate(d.data_ptr(), out.data_ptr(), len(pts), d_hint=hd.data_ptr())
+        torch.cuda.synchronize()
+        assert np.array_equal(out.cpu().numpy(), ref)
 
 
 @pytest.mark.parametrize("method", ["euler", "rk4"])
