@@ -86,6 +86,7 @@ struct mops_mesh {
     uint64_t* d_cell_key = nullptr;  // Morton key of each cell centre (particle locality order)
     double* d_cellB = nullptr;       // [C][maxv] Wachspress B_i of each cell polygon
     double* d_rloc2 = nullptr;       // [C] squared hinted-locate radius (locate_radius_kernel)
+    double* d_ring = nullptr;        // [C] hinted-locate ring distance (locate_radius_kernel)
     // grow-only scratch for mops_order_particles (not re-entrant, like the reference's global app)
     mutable void* d_scratch = nullptr;
     mutable size_t scratch_bytes = 0;
@@ -1218,8 +1219,10 @@ __device__ __forceinline__ int64_t lower_bound_u64(const uint64_t* a, int64_t n,
 }
 
 __device__ __forceinline__ void consider(const double4* cxyz, int cid, double qx, double qy, double qz, double& best,
-                                         int& bi, int exclude) {
+                                         int& bi, int exclude, const int* excl = nullptr, int n_excl = 0) {
     if (cid == exclude) return;
+    for (int k = 0; k < n_excl; ++k)
+        if (cid == excl[k]) return;
     const double4 p = cxyz[cid];
     const double d0 = qx - p.x, d1 = qy - p.y, d2 = qz - p.z;
     double dd = 0.0;
@@ -1230,7 +1233,8 @@ __device__ __forceinline__ void consider(const double4* cxyz, int cid, double qx
 // Exact nearest cell centre to q (smallest id on ties), `exclude` skipped: bucket shells
 // around q until the best distance is provably final, else an exhaustive scan.
 __device__ int nearest_centre(double qx, double qy, double qz, int64_t C, const double4* cxyz, const uint64_t* keys,
-                              const int* ids, double origin, double h, int exclude, double& best) {
+                              const int* ids, double origin, double h, int exclude, double& best,
+                              const int* excl = nullptr, int n_excl = 0) {
     best = INFINITY;
     int bi = -1;
     const int kMaxShell = 6;
@@ -1249,14 +1253,15 @@ __device__ int nearest_centre(double qx, double qy, double qz, int64_t C, const 
                         if (ix < 0 || iy < 0 || iz < 0 || ix >= kLim || iy >= kLim || iz >= kLim) continue;
                         const uint64_t key = bkey(ix, iy, iz);
                         int64_t j = lower_bound_u64(keys, C, key);
-                        for (; j < C && keys[j] == key; ++j) consider(cxyz, ids[j], qx, qy, qz, best, bi, exclude);
+                        for (; j < C && keys[j] == key; ++j)
+                            consider(cxyz, ids[j], qx, qy, qz, best, bi, exclude, excl, n_excl);
                     }
             // every point outside shells 0..s is at least s*h away
             const double bound = (double)s * h;
             if (bi >= 0 && best <= bound * bound) done = true;
         }
         if (!done) {  // far from every cell centre: exhaustive scan
-            for (int64_t cid = 0; cid < C; ++cid) consider(cxyz, (int)cid, qx, qy, qz, best, bi, exclude);
+            for (int64_t cid = 0; cid < C; ++cid) consider(cxyz, (int)cid, qx, qy, qz, best, bi, exclude, excl, n_excl);
         }
     }
     return bi;
@@ -1268,9 +1273,16 @@ __device__ int nearest_centre(double qx, double qy, double qz, int64_t C, const 
 // is the distance from h to the nearest OTHER centre, then every other centre c' has
 // |q - c'| >= d_nn - |q - h| > |q - h| + 2 m, so h is the unique exact answer and the
 // search is skipped.  Any hint (or none) gives the same result.
+//
+// A point outside that ball (near an edge of the hint's cell) is resolved among the hint
+// and its cellsOnCell neighbours S when that is provably exact: every centre outside S is
+// at least ring(h) = the distance from h's centre to the nearest centre not in S away from
+// h's centre, hence at least ring(h) - |q - h| from q; if that exceeds the best distance
+// within S by a 1 m margin, the best of S (same tie rule) is the global answer.
 __global__ void locate_kernel(int64_t n, const double* pts, int64_t C, const double4* cxyz, const uint64_t* keys,
                               const int* ids, double origin, double h, int origin_cell, const int* hint,
-                              const double* rloc2, int* out) {
+                              const double* rloc2, const double* ring, const int* cellrec, int rec_ints,
+                              int maxv, int* out) {
     const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n) return;
     const double qx = pts[3 * i], qy = pts[3 * i + 1], qz = pts[3 * i + 2];
@@ -1283,7 +1295,21 @@ __global__ void locate_kernel(int64_t n, const double* pts, int64_t C, const dou
         if (hc >= 0 && hc < C) {
             const double4 p = cxyz[hc];
             const double d0 = qx - p.x, d1 = qy - p.y, d2 = qz - p.z;
-            if (d0 * d0 + d1 * d1 + d2 * d2 < rloc2[hc]) { out[i] = hc; return; }
+            const double dh2 = d0 * d0 + d1 * d1 + d2 * d2;
+            if (dh2 < rloc2[hc]) { out[i] = hc; return; }
+            double best = INFINITY;
+            int bi = -1;
+            consider(cxyz, hc, qx, qy, qz, best, bi, -1);
+            const int* r = cellrec + (int64_t)hc * rec_ints;
+            const int nv = r[0];
+            for (int k = 0; k < nv && k < maxv; ++k) {
+                const int nb = r[1 + maxv + k];
+                if (nb >= 0) consider(cxyz, nb, qx, qy, qz, best, bi, -1);
+            }
+            if (bi >= 0 && isfinite(dh2) && ring[hc] - sqrt(dh2) > sqrt(best) * (1.0 + 1e-9) + 1.0) {
+                out[i] = bi;
+                return;
+            }
         }
     }
     double best;
@@ -1294,10 +1320,20 @@ __global__ void locate_kernel(int64_t n, const double* pts, int64_t C, const dou
 // by 1e-9 relative and 1 m absolute (>> the rounding of |q - c| at Earth radius); -1 when
 // another centre coincides with c (never taken)
 __global__ void locate_radius_kernel(int64_t C, const double4* cxyz, const uint64_t* keys, const int* ids,
-                                     double origin, double h, double* rloc2) {
+                                     double origin, double h, const int* cellrec, int rec_ints, int maxv,
+                                     double* rloc2, double* ring) {
     const int64_t c = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (c >= C) return;
     const double4 p = cxyz[c];
+    // ring(c): distance to the nearest centre outside {c} + cellsOnCell[c] (the hinted
+    // locate's local set), shrunk by 1e-9 relative and 1 m; -inf if there is none
+    {
+        const int* r = cellrec + c * rec_ints;
+        const int nv = min(r[0], maxv);
+        double b2;
+        const int o = nearest_centre(p.x, p.y, p.z, C, cxyz, keys, ids, origin, h, (int)c, b2, r + 1 + maxv, nv);
+        ring[c] = (o >= 0 && isfinite(b2)) ? sqrt(b2) * (1.0 - 1e-9) - 1.0 : -INFINITY;
+    }
     double best;
     const int nb = nearest_centre(p.x, p.y, p.z, C, cxyz, keys, ids, origin, h, (int)c, best);
     double r2 = -1.0;
@@ -1472,7 +1508,7 @@ mops_status upload(const T* h, size_t count, T** d, int64_t* acc, hipStream_t s)
 void free_mesh(mops_mesh* m) {
     if (!m) return;
     (void)hipFree(m->d_cellrec); (void)hipFree(m->d_cxyz); (void)hipFree(m->d_vxyz); (void)hipFree(m->d_cov);
-    (void)hipFree(m->d_bkeys); (void)hipFree(m->d_bcells); (void)hipFree(m->d_cell_key); (void)hipFree(m->d_cellB); (void)hipFree(m->d_rloc2);
+    (void)hipFree(m->d_bkeys); (void)hipFree(m->d_bcells); (void)hipFree(m->d_cell_key); (void)hipFree(m->d_cellB); (void)hipFree(m->d_rloc2); (void)hipFree(m->d_ring);
     (void)hipFree(m->d_scratch);
     delete m;
 }
@@ -1652,8 +1688,10 @@ mops_status mops_mesh_create(const mops_mesh_desc* desc, void* stream, mops_mesh
     if ((st = dmalloc(&m->d_cell_key, (size_t)C, &acc)) != MOPS_OK) { free_mesh(m); return st; }
     cell_key_kernel<<<grid_for(C), kBlock, 0, s>>>(C, m->d_cxyz, m->d_cell_key);
     if ((st = dmalloc(&m->d_rloc2, (size_t)C, &acc)) != MOPS_OK) { free_mesh(m); return st; }
+    if ((st = dmalloc(&m->d_ring, (size_t)C, &acc)) != MOPS_OK) { free_mesh(m); return st; }
     locate_radius_kernel<<<grid_for(C), kBlock, 0, s>>>(C, m->d_cxyz, m->d_bkeys, m->d_bcells, m->bucket_origin,
-                                                        m->bucket_h, m->d_rloc2);
+                                                        m->bucket_h, m->d_cellrec, m->rec_ints, m->maxv,
+                                                        m->d_rloc2, m->d_ring);
     if ((st = dmalloc(&m->d_cellB, (size_t)(C * m->maxv), &acc)) != MOPS_OK) { free_mesh(m); return st; }
     switch (m->maxv) {
         case 7: cell_b_kernel<7><<<grid_for(C), kBlock, 0, s>>>(C, m->d_cellrec, m->d_vxyz, m->d_cellB); break;
@@ -1860,7 +1898,7 @@ mops_status mops_locate_cells(const mops_mesh* mesh, int64_t n, const double* d_
     hipStream_t s = (hipStream_t)stream;
     locate_kernel<<<grid_for(n), kBlock, 0, s>>>(n, d_points, mesh->C, mesh->d_cxyz, mesh->d_bkeys, mesh->d_bcells,
                                                  mesh->bucket_origin, mesh->bucket_h, mesh->origin_cell, nullptr,
-                                                 nullptr, d_cells);
+                                                 nullptr, nullptr, nullptr, 0, 0, d_cells);
     HIP_TRY(hipGetLastError());
     return MOPS_OK;
 }
@@ -1873,7 +1911,8 @@ mops_status mops_locate_cells_hinted(const mops_mesh* mesh, int64_t n, const dou
     hipStream_t s = (hipStream_t)stream;
     locate_kernel<<<grid_for(n), kBlock, 0, s>>>(n, d_points, mesh->C, mesh->d_cxyz, mesh->d_bkeys, mesh->d_bcells,
                                                  mesh->bucket_origin, mesh->bucket_h, mesh->origin_cell, d_hint,
-                                                 d_hint ? mesh->d_rloc2 : nullptr, d_cells);
+                                                 mesh->d_rloc2, mesh->d_ring, mesh->d_cellrec, mesh->rec_ints,
+                                                 mesh->maxv, d_cells);
     HIP_TRY(hipGetLastError());
     return MOPS_OK;
 }
