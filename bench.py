@@ -68,6 +68,9 @@ def parse():
     p.add_argument("--backend", choices=["nccl", "gloo"], default="nccl",
                    help="collective backend for N > 1 (nccl = RCCL over xGMI; gloo only to rehearse the multi-rank "
                         "path on one GPU with MOPS_BENCH_ONE_DEVICE=1)")
+    p.add_argument("--segment", type=int, default=0,
+                   help="integration steps per kernel launch (whole record periods; 0 = the whole run at N=1, "
+                        "a quarter of it at N>1 so record all-gathers overlap the next launch)")
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--cpu-seconds", type=float, default=12.0, help="target CPU-baseline sample length")
     return p.parse_args()
@@ -190,7 +193,15 @@ def main():
     seed_cells = ps.original(ps.cell).cpu().numpy()
     period = ps.record_period(pathline=pathline)
     n_steps = cfg.n_steps
-    bounds = list(range(0, n_steps, period)) + [n_steps]
+    # launches: the whole run at N=1 (every launch re-reads the particle state and re-loads
+    # each particle's cell stencil: 30-step launches cost 6% at config 2); at N>1 quarters of
+    # the run, whose records are all-gathered while the next quarter computes, and a final
+    # one-record launch so that only one record's gather is exposed
+    seg = args.segment if args.segment > 0 else (n_steps if world == 1 else period * max(1, ps.K // 4))
+    seg = max(period, (seg // period) * period)  # whole record periods per launch
+    bounds = list(range(0, n_steps, seg)) + [n_steps]
+    if args.segment <= 0 and world > 1 and bounds[-1] - bounds[-2] > period:
+        bounds.insert(-1, bounds[-1] - period)
     segments = [(bounds[i], bounds[i + 1]) for i in range(len(bounds) - 1)]
     compute = torch.cuda.Stream(dev)
     comm = torch.cuda.Stream(dev)
@@ -215,14 +226,15 @@ def main():
                 if timed:
                     e1.record(compute)
                     kernel_ms.append((e0, e1))
-                if world > 1:
-                    k = s1 // period - 1
-                    if 0 <= k < ps.K:
+                if world > 1:  # the records this segment completed, gathered while the next one computes
+                    k0, k1 = s0 // period, min(s1 // period, ps.K)
+                    if k1 > k0:
                         done = torch.cuda.Event()
                         done.record(compute)
                         comm.wait_event(done)
                         with torch.cuda.stream(comm):
-                            all_gather_flat(dist, gathered[k].view(-1), ps.records[k].view(-1), args.backend)
+                            for k in range(k0, k1):
+                                all_gather_flat(dist, gathered[k].view(-1), ps.records[k].view(-1), args.backend)
         compute.synchronize()
         comm.synchronize()
 
@@ -261,7 +273,8 @@ def main():
     B = algorithmic_bytes_per_pstep(nv_mean, mesh.nVertLevels, 2 if pathline else 1)
     psteps_per_launch = attempted / len(segments)
     achieved = B * psteps_per_launch / avg_kernel_s / 1e9
-    traffic, measured = measured_traffic(f"ec30to60_{args.mode}_{args.method}_{args.particles}", avg_kernel_s)
+    traffic, measured = measured_traffic(f"ec30to60_{args.mode}_{args.method}_{args.particles}_seg{seg}",
+                                         avg_kernel_s)
 
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
@@ -389,7 +402,7 @@ def main_chain(args, mesh, dev, world, rank):
     def one_call(timed):
         res = chain.run(seeds, depth=args.depth, method=1 if args.method == "euler" else 0, delta_t=args.dt,
                         record_t=args.record, keep_lines=False, compute_stream=compute, on_pair=on_pair,
-                        timing=timing if timed else None)
+                        timing=timing if timed else None, segment_steps=args.segment)
         compute.synchronize(); comm.synchronize()
         return res
 
@@ -424,7 +437,9 @@ def main_chain(args, mesh, dev, world, rank):
     psteps_per_launch = attempted / args.steps / launches_per_call
     achieved = B * psteps_per_launch / avg_kernel_s / 1e9
     mesh_class = "EC30to60" if args.config == 3 else "oRRS18to6"
-    traffic, measured = measured_traffic(f"{mesh_class.lower()}_chain{args.config}_{args.method}_{args.particles}",
+    seg_key = args.segment if args.segment > 0 else args.duration // args.dt
+    traffic, measured = measured_traffic(f"{mesh_class.lower()}_chain{args.config}_{args.method}_{args.particles}"
+                                         f"_seg{seg_key}",
                                          avg_kernel_s)
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:

@@ -55,14 +55,16 @@ class PathlineChain:
 
     def run(self, seeds, depth: float, particle_depths=None, method: int = L.MOPS_EULER, delta_t: int = 60,
             record_t: int = 360, direction: int = L.MOPS_FORWARD, follow_last: bool = True, keep_lines: bool = True,
-            compute_stream=None, on_pair=None, timing=None):
+            compute_stream=None, on_pair=None, timing=None, segment_steps: int = 0):
         """Run all pairs; returns device tensors {points, velocity, temperature,
         salinity, lastPoint, death_step (of the last pair)} when ``keep_lines``,
         else only lastPoint/death_step.  ``on_pair(p, last)`` is called after pair p
         is enqueued (timing / record gathers); ``timing`` (a list) receives an
         (start, end) HIP event pair around every trajectory launch.
         ``attempted`` in the result counts particle-steps whose velocity
-        evaluation ran, summed over pairs (device scalar)."""
+        evaluation ran, summed over pairs (device scalar).  ``segment_steps``: integration
+        steps per kernel launch, rounded to whole record periods (0 = one launch per pair:
+        every launch re-reads the particle state and re-loads each particle's cell stencil)."""
         import torch
         dev = self.device or torch.device("cuda", torch.cuda.current_device())
         cs = compute_stream or torch.cuda.current_stream(dev)
@@ -109,11 +111,12 @@ class PathlineChain:
                 # a continuation pair: each particle's current cell is an exact-locate hint
                 ps.reseed(s, d, stream=cs.cuda_stream, hint_cells=(p > 0 and follow_last))
                 front, back = fields[p], fields[p + 1]
-                for s0 in range(0, cfg.n_steps, period):
+                seg = cfg.n_steps if segment_steps <= 0 else max(period, (segment_steps // period) * period)
+                for s0 in range(0, cfg.n_steps, seg):
                     if timing is not None:
                         e0 = torch.cuda.Event(enable_timing=True); e1 = torch.cuda.Event(enable_timing=True)
                         e0.record(cs)
-                    ps.advance(front, back, s0, min(s0 + period, cfg.n_steps), stream=cs.cuda_stream)
+                    ps.advance(front, back, s0, min(s0 + seg, cfg.n_steps), stream=cs.cuda_stream)
                     if timing is not None:
                         e1.record(cs)
                         timing.append((e0, e1))

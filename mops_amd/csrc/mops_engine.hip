@@ -1412,21 +1412,31 @@ __global__ void cell_b_kernel(int64_t C, const int* cellrec, const double4* vxyz
     }
 }
 
-__global__ void pair_record_kernel(int64_t V, int L, const double* zt, const double* vel, const double* w,
-                                   double* pr) {
-    const int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (idx >= V * (L - 1)) return;
-    const int64_t v = idx / (L - 1);
-    const int k = (int)(idx % (L - 1)) + 1;
-    double2* o = reinterpret_cast<double2*>(pr + idx * kPairRec);
-    const double* z = zt + v * L;
-    const double* ww = w + v * (L + 1);
-    const double* u = vel + (v * L + k - 1) * 3;
-    o[0] = make_double2(z[k - 1], z[k]);
-    o[1] = make_double2(ww[k - 1], ww[k]);
-    o[2] = make_double2(u[0], u[1]);
-    o[3] = make_double2(u[2], u[3]);
-    o[4] = make_double2(u[4], u[5]);
+// Level-pair records (mops_field::d_pr), one 16-B chunk per thread so that a wave's
+// stores are contiguous: chunk q of record (v, k) is {z_{k-1}, z_k}, {w_{k-1}, w_k} or
+// two of the six doubles vel_{k-1}.xyz, vel_k.xyz.  IDX = uint32_t when the chunk count fits.
+template <typename IDX>
+__global__ void pair_record_kernel(int64_t V, int L, const double* __restrict__ zt, const double* __restrict__ vel,
+                                   const double* __restrict__ w, double* __restrict__ pr) {
+    const IDX j = (IDX)blockIdx.x * (IDX)blockDim.x + (IDX)threadIdx.x;
+    const IDX lm1 = (IDX)(L - 1);
+    if ((int64_t)j >= V * (L - 1) * (kPairRec / 2)) return;
+    const IDX rec = j / (IDX)(kPairRec / 2);
+    const int q = (int)(j - rec * (IDX)(kPairRec / 2));
+    const IDX v = rec / lm1;
+    const int k = (int)(rec - v * lm1) + 1;
+    double2 val;
+    if (q == 0) {
+        const double* z = zt + (int64_t)v * L;
+        val = make_double2(z[k - 1], z[k]);
+    } else if (q == 1) {
+        const double* ww = w + (int64_t)v * (L + 1);
+        val = make_double2(ww[k - 1], ww[k]);
+    } else {
+        const double* u = vel + ((int64_t)v * L + k - 1) * 3 + 2 * (q - 2);
+        val = make_double2(u[0], u[1]);
+    }
+    reinterpret_cast<double2*>(pr)[j] = val;
 }
 
 __device__ __forceinline__ uint64_t spread3(uint64_t v) {  // 21 bits -> every third bit
@@ -1715,7 +1725,15 @@ static mops_status compute_mono(const mops_mesh* mesh, mops_field* f, hipStream_
     if (!f->d_pr) MOPS_TRY(dmalloc(&f->d_pr, (size_t)((npr + 1) * kPairRec), &f->bytes));
     HIP_TRY(hipMemsetAsync(f->d_pr + npr * kPairRec, 0, kPairRec * sizeof(double), s));
     if (npr > 0)
-        pair_record_kernel<<<grid_for(npr), kBlock, 0, s>>>(mesh->V, mesh->L, f->d_zt, f->d_vel, f->d_w, f->d_pr);
+    {
+        const int64_t chunks = npr * (kPairRec / 2);
+        if (chunks < ((int64_t)1 << 32) - kBlock)
+            pair_record_kernel<uint32_t><<<grid_for(chunks), kBlock, 0, s>>>(mesh->V, mesh->L, f->d_zt, f->d_vel,
+                                                                           f->d_w, f->d_pr);
+        else
+            pair_record_kernel<uint64_t><<<grid_for(chunks), kBlock, 0, s>>>(mesh->V, mesh->L, f->d_zt, f->d_vel,
+                                                                           f->d_w, f->d_pr);
+    }
     if (!f->d_mono) MOPS_TRY(dmalloc(&f->d_mono, (size_t)mesh->C, &f->bytes));
     if (!f->d_vmono) MOPS_TRY(dmalloc(&f->d_vmono, (size_t)mesh->V, &f->bytes));
     HIP_TRY(hipMemsetAsync(f->d_vmono, 1, (size_t)mesh->V, s));
