@@ -69,8 +69,9 @@ def parse():
                    help="collective backend for N > 1 (nccl = RCCL over xGMI; gloo only to rehearse the multi-rank "
                         "path on one GPU with MOPS_BENCH_ONE_DEVICE=1)")
     p.add_argument("--segment", type=int, default=0,
-                   help="integration steps per kernel launch (whole record periods; 0 = the whole run at N=1, "
-                        "a quarter of it at N>1 so record all-gathers overlap the next launch)")
+                   help="integration steps per kernel launch (config 2: whole record periods; 0 = the whole "
+                        "run at N=1, a quarter of it at N>1 so record all-gathers overlap the next launch; "
+                        "chains: 0 = launches of 3 simulated days with a locality re-sort between them)")
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--cpu-seconds", type=float, default=12.0, help="target CPU-baseline sample length")
     return p.parse_args()
@@ -402,7 +403,7 @@ def main_chain(args, mesh, dev, world, rank):
     def one_call(timed):
         res = chain.run(seeds, depth=args.depth, method=1 if args.method == "euler" else 0, delta_t=args.dt,
                         record_t=args.record, keep_lines=False, compute_stream=compute, on_pair=on_pair,
-                        timing=timing if timed else None, segment_steps=args.segment)
+                        timing=timing if timed else None, segment_steps=args.segment if args.segment else -1)
         compute.synchronize(); comm.synchronize()
         return res
 
@@ -437,7 +438,8 @@ def main_chain(args, mesh, dev, world, rank):
     psteps_per_launch = attempted / args.steps / launches_per_call
     achieved = B * psteps_per_launch / avg_kernel_s / 1e9
     mesh_class = "EC30to60" if args.config == 3 else "oRRS18to6"
-    seg_key = args.segment if args.segment > 0 else args.duration // args.dt
+    from mops_amd.chain import REORDER_SECONDS
+    seg_key = args.segment if args.segment > 0 else min(args.duration // args.dt, REORDER_SECONDS // args.dt)
     traffic, measured = measured_traffic(f"{mesh_class.lower()}_chain{args.config}_{args.method}_{args.particles}"
                                          f"_seg{seg_key}",
                                          avg_kernel_s)

@@ -28,6 +28,7 @@ from . import _lib as L
 from .engine import DeviceField, DeviceMesh, ParticleSet, TrajectoryConfig
 
 EARTH_RADIUS_M = 6_371_000.0  # pyMOPSAPI.py:46
+REORDER_SECONDS = 3 * 86400  # default launch length of long pairs (simulated time), see PathlineChain.run
 
 
 class PathlineChain:
@@ -55,7 +56,7 @@ class PathlineChain:
 
     def run(self, seeds, depth: float, particle_depths=None, method: int = L.MOPS_EULER, delta_t: int = 60,
             record_t: int = 360, direction: int = L.MOPS_FORWARD, follow_last: bool = True, keep_lines: bool = True,
-            compute_stream=None, on_pair=None, timing=None, segment_steps: int = 0):
+            compute_stream=None, on_pair=None, timing=None, segment_steps: int = -1, reorder: bool = True):
         """Run all pairs; returns device tensors {points, velocity, temperature,
         salinity, lastPoint, death_step (of the last pair)} when ``keep_lines``,
         else only lastPoint/death_step.  ``on_pair(p, last)`` is called after pair p
@@ -63,8 +64,11 @@ class PathlineChain:
         (start, end) HIP event pair around every trajectory launch.
         ``attempted`` in the result counts particle-steps whose velocity
         evaluation ran, summed over pairs (device scalar).  ``segment_steps``: integration
-        steps per kernel launch, rounded to whole record periods (0 = one launch per pair:
-        every launch re-reads the particle state and re-loads each particle's cell stencil)."""
+        steps per kernel launch (0 = one launch per pair: every launch re-reads the particle
+        state and re-loads each particle's cell stencil; -1 = one launch per REORDER_SECONDS
+        of simulated time).  ``reorder``: restore the particles' locality order between
+        launches (long pairs: particles drift across many cells and a wave's lanes stop
+        sharing stencils -- config 5's 30-day pairs run 9% faster re-sorted every 3 days)."""
         import torch
         dev = self.device or torch.device("cuda", torch.cuda.current_device())
         cs = compute_stream or torch.cuda.current_stream(dev)
@@ -111,11 +115,16 @@ class PathlineChain:
                 # a continuation pair: each particle's current cell is an exact-locate hint
                 ps.reseed(s, d, stream=cs.cuda_stream, hint_cells=(p > 0 and follow_last))
                 front, back = fields[p], fields[p + 1]
-                seg = cfg.n_steps if segment_steps <= 0 else max(period, (segment_steps // period) * period)
+                if segment_steps < 0:
+                    seg = max(1, REORDER_SECONDS // int(delta_t))
+                else:
+                    seg = cfg.n_steps if segment_steps == 0 else int(segment_steps)  # records by absolute step
                 for s0 in range(0, cfg.n_steps, seg):
                     if timing is not None:
                         e0 = torch.cuda.Event(enable_timing=True); e1 = torch.cuda.Event(enable_timing=True)
                         e0.record(cs)
+                    if reorder and s0 > 0:
+                        ps.reorder(stream=cs.cuda_stream)
                     ps.advance(front, back, s0, min(s0 + seg, cfg.n_steps), stream=cs.cuda_stream)
                     if timing is not None:
                         e1.record(cs)
