@@ -363,7 +363,13 @@ def main_chain(args, mesh, dev, world, rank):
     else:
         from mops_amd.synth_device import DeviceFieldRecycler, DeviceSnapshotSource
         src = DeviceSnapshotSource(mesh, dev)
-        chain = PathlineChain(dmesh, DeviceFieldRecycler(dmesh, src), n_snap, gap_seconds=args.duration,
+        recycler = DeviceFieldRecycler(dmesh, src)
+        # the two field buffers are allocated before the timed region (hipMalloc of ~2 x 75 GB is
+        # setup); every snapshot a call uses is still generated and derived inside it
+        for i in range(2):
+            recycler.release(recycler(i, torch.cuda.current_stream(dev).cuda_stream))
+        torch.cuda.synchronize()
+        chain = PathlineChain(dmesh, recycler, n_snap, gap_seconds=args.duration,
                               device=dev, own_fields=True, prefetch=False)
     if args.config == 4:  # strong scaling: 1e7 particles in total, one contiguous shard per rank
         allseeds = make_seeds(args.particles, 0)

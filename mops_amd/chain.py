@@ -90,7 +90,7 @@ class PathlineChain:
         with torch.cuda.stream(cs):
             fields[0] = self.make_field(0, cs.cuda_stream)
             fields[1] = self.make_field(1, cs.cuda_stream)
-            ps = ParticleSet(self.mesh, seeds0.cpu().numpy(), cfg.depth, cfg, device=dev)
+            ps = ParticleSet(self.mesh, seeds0, cfg.depth, cfg, device=dev)
         period = ps.record_period(pathline=True)
         pts_acc, vel_acc, tmp_acc, sal_acc = [], [], [], []
         last = None
@@ -161,7 +161,10 @@ class PathlineChain:
         if self.own_fields:
             cs.synchronize()
             for f in fields.values():
-                f.close()
+                if hasattr(self.make_field, "release"):
+                    self.make_field.release(f)  # kept for the next run (e.g. DeviceFieldRecycler)
+                else:
+                    f.close()
         with torch.cuda.stream(cs):
             res = dict(lastPoint=last, death_step=ps.original(ps.death), attempted=attempted)
             if keep_lines:

@@ -242,7 +242,10 @@ class ParticleSet:
         self.use_order = use_order
         self.torch = torch
         dev = device or torch.device("cuda", torch.cuda.current_device())
-        s = torch.as_tensor(np.ascontiguousarray(seeds_xyz, dtype=np.float64).reshape(-1, 3), device=dev)
+        if isinstance(seeds_xyz, torch.Tensor):  # already resident: no host round trip
+            s = seeds_xyz.to(device=dev, dtype=torch.float64).reshape(-1, 3).clone()
+        else:
+            s = torch.as_tensor(np.ascontiguousarray(seeds_xyz, dtype=np.float64).reshape(-1, 3), device=dev)
         self.n = int(s.shape[0])
         self.mesh = mesh
         self.cfg = cfg

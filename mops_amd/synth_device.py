@@ -65,7 +65,11 @@ class DeviceFieldRecycler:
     * ``prepare(i)`` generates snapshot i's raw arrays on a side stream, so it
       overlaps the running pair (one raw set, reused once its last reader is done);
     * ``refill(field, i, stream)`` re-derives the finished pair's field in place
-      from them (mops_field_rebuild_device): no allocation, no host sync.
+      from them (mops_field_rebuild_device): no allocation, no host sync;
+    * ``release(field)`` keeps a field the chain no longer needs for the next
+      ``self(i, stream)``, which then re-derives it instead of allocating (field
+      buffers are ~75 GB on an oRRS18to6-class mesh: their hipMalloc is setup,
+      not per-run work).
     """
 
     def __init__(self, dmesh, source: DeviceSnapshotSource, phase_per_snapshot: float = 0.35):
@@ -79,10 +83,18 @@ class DeviceFieldRecycler:
         self.raw_i = None
         self.ready = None
         self.consumed = None
+        self.pool = []
+
+    def release(self, field):
+        self.pool.append(field)
 
     def __call__(self, i, stream):
         from .engine import DeviceField
         torch = self.torch
+        if self.pool:
+            ts = torch.cuda.ExternalStream(stream) if isinstance(stream, int) and stream else \
+                torch.cuda.current_stream(self.source.device)
+            return self.refill(self.pool.pop(), i, ts)
         snap = self.source.make(timestep=i, phase=self.phase * i)
         torch.cuda.current_stream(self.source.device).synchronize()
         f = DeviceField.from_device_snapshot(self.dmesh, snap, timestep=i, stream=stream)
