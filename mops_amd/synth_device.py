@@ -1,16 +1,15 @@
 """Synthetic snapshot fields generated directly in HBM.
 
 Same analytic flow as :func:`mops_amd.synth.make_snapshot` (solid body +
-travelling wave-3, depth decay, w on the interface grid), evaluated with torch
-on the GPU, so long pathline chains on oRRS18to6-class meshes (3.5M cells x
+travelling wave-3, depth decay, w on the interface grid), evaluated on the GPU
+by one HIP kernel (mops_amd/csrc/mops_synth.hip -> lib/libmops_synth.so), so
+long pathline chains on oRRS18to6-class meshes (3.5M cells x
 80 levels: 2.2 GB per raw field) can stream dozens of daily snapshots through
 ``mops_field_create_device`` without building them on the host.  Values agree
 with the numpy generator to rounding (libm vs device sin/cos); the parity
 tests use the numpy generator, this module only feeds the configs 4/5 bench.
 """
 from __future__ import annotations
-
-import math
 
 import numpy as np
 
@@ -32,30 +31,41 @@ class DeviceSnapshotSource:
         self.u0, self.u1, self.w0 = u0, u1, w0
 
     def make(self, timestep: int = 0, phase: float = 0.0) -> dict:
+        """One snapshot's raw arrays, generated on the current stream by libmops_synth.so
+        (mops_amd/csrc/mops_synth.hip: one pass per cell)."""
+        import ctypes as C
         torch = self.torch
-        lat, lon, H = self.lat, self.lon, self.H
-        bot = H - 0.5 * (H - 2000.0) * (1.0 + torch.sin(2.0 * lat) * torch.cos(3.0 * lon)) * 0.5
-        bot = torch.clamp(bot, 1500.0, H)
-        ssh = 0.5 * torch.cos(lat) * torch.sin(2.0 * lon + phase)
-        thick = self.ref_dz[None, :] * ((bot + ssh) / H)[:, None]
-        # prefix sum over levels as an outer-dimension scan ([L, C]: one coalesced column per cell);
-        # torch's innermost-dimension scan over 80 levels is ~30x slower on this shape
-        csum = torch.cumsum(thick.t().contiguous(), dim=0).t()
-        zmid = csum - 0.5 * thick
-        decay = torch.exp(-zmid / 1500.0)
-        del zmid
-        cl = torch.cos(lat)[:, None]
-        u = (self.u0 * cl + self.u1 * torch.cos(3.0 * lon - phase)[:, None] * torch.sin(2.0 * lat)[:, None] * cl) * decay
-        v = (self.u1 * torch.sin(3.0 * lon - phase)[:, None] * cl * cl) * decay
-        del decay
-        zi = torch.cat([torch.zeros((lat.shape[0], 1), dtype=torch.float64, device=self.device), csum], dim=1)
-        del csum
-        wv = (self.w0 * torch.sin(2.0 * lat)[:, None] * torch.sin(math.pi * zi / zi[:, -1:])
-              * torch.cos(lon - phase)[:, None])
-        del zi
-        return {"layerThickness": thick.contiguous(), "bottomDepth": bot.contiguous(),
-                "zonalVelocity": u.contiguous(), "meridionalVelocity": v.contiguous(),
-                "vertVelocityTop": wv.contiguous(), "timestep": int(timestep)}
+        n, L, dev = int(self.lat.shape[0]), self.L, self.device
+        out = {k: torch.empty(shape, dtype=torch.float64, device=dev) for k, shape in
+               (("layerThickness", (n, L)), ("bottomDepth", (n,)), ("zonalVelocity", (n, L)),
+                ("meridionalVelocity", (n, L)), ("vertVelocityTop", (n, L + 1)))}
+        P = C.c_void_p
+        rc = _synth_lib().mops_synth_snapshot(
+            C.c_int64(n), C.c_int(L), P(self.lat.data_ptr()), P(self.lon.data_ptr()), P(self.ref_dz.data_ptr()),
+            C.c_double(self.H), C.c_double(phase), C.c_double(self.u0), C.c_double(self.u1), C.c_double(self.w0),
+            P(out["layerThickness"].data_ptr()), P(out["bottomDepth"].data_ptr()), P(out["zonalVelocity"].data_ptr()),
+            P(out["meridionalVelocity"].data_ptr()), P(out["vertVelocityTop"].data_ptr()),
+            P(torch.cuda.current_stream(dev).cuda_stream))
+        if rc != 0:
+            raise RuntimeError("mops_synth_snapshot failed")
+        out["timestep"] = int(timestep)
+        return out
+
+
+_SYNTH = None
+
+
+def _synth_lib():
+    """libmops_synth.so (built in-tree by __graft_entry__.build_synth)."""
+    global _SYNTH
+    if _SYNTH is None:
+        import ctypes
+        import os
+        path = os.path.join(os.path.dirname(os.path.abspath(__file__)), "lib", "libmops_synth.so")
+        if not os.path.exists(path):
+            raise RuntimeError(f"{path} is missing: run __graft_entry__.build()")
+        _SYNTH = ctypes.CDLL(path)
+    return _SYNTH
 
 
 class DeviceFieldRecycler:
