@@ -128,3 +128,32 @@ def test_config3_full_size_pair(ec_case, oracle_lib):
                          euler=True, cells=cells[idx])
     _check_sample(lines, death, idx, ref, pathline=True)
     _check_shells(lines, death)
+
+
+def test_config3_full_size_chain(ec_case, oracle_lib):
+    """Config-3 shape through the pair-chaining driver (3 daily snapshots = 2 pairs, 1e6 particles):
+    continuation seeds, the exact hinted seed location between pairs and the line concatenation at
+    full mesh size.  Particles are independent across pairs too, so a sample's oracle chain (run on
+    the sampled seeds alone) must reproduce the sampled lines bit for bit."""
+    import torch
+    import bench
+    from test_chain import oracle_chain
+    from mops_amd import synth
+    from mops_amd.chain import PathlineChain
+    mesh, dm, f0, f1, _, _ = ec_case
+    snaps = [synth.make_snapshot(mesh, timestep=0), synth.make_snapshot(mesh, timestep=1, phase=0.35),
+             synth.make_snapshot(mesh, timestep=2, phase=0.7)]
+    from mops_amd.engine import DeviceField
+    f2 = DeviceField.from_snapshot(dm, snaps[2])
+    fields = [f0, f1, f2]
+    depth = bench.layer_mid_depth(mesh, 10)
+    seeds = bench.make_seeds(1_000_000, 0)
+    chain = PathlineChain(dm, lambda i, stream: fields[i], 3, gap_seconds=86400, own_fields=False)
+    got = chain.run(seeds, depth=depth, method=1, delta_t=60, record_t=3600)
+    torch.cuda.synchronize()
+    rng = np.random.default_rng(3)
+    idx = np.sort(rng.choice(len(seeds), 160, replace=False))
+    ref = oracle_chain(oracle_lib, mesh, snaps, seeds[idx], depth, None, 86400, 60, 3600, euler=True)
+    ti = torch.as_tensor(idx, device=got["points"].device)
+    for k in ("points", "velocity", "temperature", "salinity", "lastPoint"):
+        assert np.array_equal(got[k][ti].cpu().numpy(), ref[k]), k
