@@ -125,6 +125,24 @@ def test_streamline_parity(dev_small, ref_small, small_case, oracle_lib, method,
 
 
 @pytest.mark.parametrize("method", ["euler", "rk4"])
+def test_pathline_backward_parity(dev_small, ref_small, small_case, oracle_lib, method):
+    """PathLine with directionType backward (signed deltaT, Q7) through the alpha ramp and RK4 stage alphas."""
+    from mops_amd import synth
+    from mops_amd.engine import TrajectoryConfig, run_trajectories
+    mesh, _, _ = small_case
+    dm, f0, f1 = dev_small
+    r0, r1 = ref_small
+    seeds = synth.uniform_band_seeds(400, seed=15)
+    cfg = TrajectoryConfig(deltaT=300, simulationDuration=43200, recordT=3600, depth=450.0,
+                           method=1 if method == "euler" else 0, direction=1)
+    got = run_trajectories(dm, f0, f1, cfg, seeds)
+    ref = oracle_lib.run(mesh, r0, r1, seeds, depth=450.0, delta_t=300, duration=43200, record_t=3600,
+                         euler=(method == "euler"), backward=True, cells=got["cells"])
+    assert_lines_match(got, ref, f"pathline backward {method}")
+    assert np.array_equal(got["points"], ref["points"])
+
+
+@pytest.mark.parametrize("method", ["euler", "rk4"])
 def test_pathline_parity(dev_small, ref_small, small_case, oracle_lib, method):
     from mops_amd import synth
     from mops_amd.engine import TrajectoryConfig, run_trajectories
