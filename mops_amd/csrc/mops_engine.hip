@@ -210,6 +210,9 @@ struct Cell {
     int vid[MAXV];
     int V;              // vertex count (index of the all-zero level-pair record is V*(L-1))
     bool rc;            // compile-time constant per kernel (load_cell<MAXV, RC>): which members below are live
+    // polygon positions in "rotated" order: x[0] = poly[nv-1], x[j] = poly[j-1] (1 <= j < nv), so
+    // that edge k (poly[k-1], poly[k]) and the reference's running triangle A_k = area(poly[k-1],
+    // poly[k], p) are the slot pair (k, k+1), wrapping to slot 0 only at k = nv-1
     double x[MAXV], y[MAXV], z[MAXV];
     double B[MAXV];  // Wachspress B_i = area(poly[i-1], poly[i], poly[i+1]) (depends on the polygon only)
     const double4* __restrict__ vxyz;   // rc == false: polygon re-read per evaluation (L1-resident)
@@ -242,34 +245,38 @@ __device__ __forceinline__ void load_cell(Cell<MAXV>& c, int cell, const int* __
 #pragma unroll
     for (int k = 0; k < MAXV; ++k) c.vid[k] = buf[1 + k];
     if constexpr (RC) {
+        double px[MAXV], py[MAXV], pz[MAXV];  // natural order
 #pragma unroll
         for (int k = 0; k < MAXV; ++k) {
             if (k < nv) {
                 const double4 p = vxyz[c.vid[k]];
-                c.x[k] = p.x; c.y[k] = p.y; c.z[k] = p.z;
+                px[k] = p.x; py[k] = p.y; pz[k] = p.z;
             } else {
-                c.x[k] = 0.0; c.y[k] = 0.0; c.z[k] = 0.0;
+                px[k] = 0.0; py[k] = 0.0; pz[k] = 0.0;
             }
         }
         double lx = 0, ly = 0, lz = 0;  // poly[nv-1]
 #pragma unroll
         for (int k = 0; k < MAXV; ++k)
-            if (k == nv - 1) { lx = c.x[k]; ly = c.y[k]; lz = c.z[k]; }
+            if (k == nv - 1) { lx = px[k]; ly = py[k]; lz = pz[k]; }
 #pragma unroll
         for (int i = 0; i < MAXV; ++i) {
             if (i < nv) {
-                const double qx = (i == 0) ? lx : c.x[(i + MAXV - 1) % MAXV];
-                const double qy = (i == 0) ? ly : c.y[(i + MAXV - 1) % MAXV];
-                const double qz = (i == 0) ? lz : c.z[(i + MAXV - 1) % MAXV];
+                const double qx = (i == 0) ? lx : px[(i + MAXV - 1) % MAXV];
+                const double qy = (i == 0) ? ly : py[(i + MAXV - 1) % MAXV];
+                const double qz = (i == 0) ? lz : pz[(i + MAXV - 1) % MAXV];
                 const bool wrap = (i + 1 >= nv);
-                const double nx = wrap ? c.x[0] : c.x[(i + 1) % MAXV];
-                const double ny = wrap ? c.y[0] : c.y[(i + 1) % MAXV];
-                const double nz = wrap ? c.z[0] : c.z[(i + 1) % MAXV];
-                c.B[i] = tri_area(qx, qy, qz, c.x[i], c.y[i], c.z[i], nx, ny, nz);
+                const double nx = wrap ? px[0] : px[(i + 1) % MAXV];
+                const double ny = wrap ? py[0] : py[(i + 1) % MAXV];
+                const double nz = wrap ? pz[0] : pz[(i + 1) % MAXV];
+                c.B[i] = tri_area(qx, qy, qz, px[i], py[i], pz[i], nx, ny, nz);
             } else {
                 c.B[i] = 0.0;
             }
         }
+        c.x[0] = lx; c.y[0] = ly; c.z[0] = lz;
+#pragma unroll
+        for (int j = 1; j < MAXV; ++j) { c.x[j] = px[j - 1]; c.y[j] = py[j - 1]; c.z[j] = pz[j - 1]; }
     } else {
         c.vxyz = vxyz;
         c.cellB = cellB;
@@ -285,56 +292,62 @@ __device__ __forceinline__ bool weights(const Cell<MAXV>& c, int L, int V, doubl
     const int nv = c.nv;
     if (nv <= 0 || nv > kMaxVertex) return false;
     if (!isfinite(px) || !isfinite(py) || !isfinite(pz)) return false;
+    // rotated slots (see Cell): X[0] = poly[nv-1], X[j] = poly[j-1]
     double X[MAXV], Y[MAXV], Z[MAXV], BB[MAXV];
+    int vlast = 0;  // non-cached polygon: vertex id of poly[nv-1]
+    if (!c.rc) {
 #pragma unroll
-    for (int k = 0; k < MAXV; ++k) {
+        for (int k = 0; k < MAXV; ++k)
+            if (k == nv - 1) vlast = c.vid[k];
+    }
+#pragma unroll
+    for (int j = 0; j < MAXV; ++j) {
         if (c.rc) {
-            X[k] = c.x[k]; Y[k] = c.y[k]; Z[k] = c.z[k]; BB[k] = c.B[k];
-        } else if (k < nv) {
-            const double4 q = c.vxyz[c.vid[k]];
-            X[k] = q.x; Y[k] = q.y; Z[k] = q.z;
-            BB[k] = c.cellB[(int64_t)c.id * MAXV + k];
+            X[j] = c.x[j]; Y[j] = c.y[j]; Z[j] = c.z[j]; BB[j] = c.B[j];
         } else {
-            X[k] = 0.0; Y[k] = 0.0; Z[k] = 0.0; BB[k] = 0.0;
+            if (j < nv) {
+                const double4 q = c.vxyz[j == 0 ? vlast : c.vid[(j + MAXV - 1) % MAXV]];
+                X[j] = q.x; Y[j] = q.y; Z[j] = q.z;
+                BB[j] = c.cellB[(int64_t)c.id * MAXV + j];
+            } else {
+                X[j] = 0.0; Y[j] = 0.0; Z[j] = 0.0; BB[j] = 0.0;
+            }
         }
     }
-#pragma unroll
-    for (int k = 0; k < MAXV; ++k) {
-        if (k < nv) {
-            const bool wrap = (k + 1 >= nv);
-            const double bx = wrap ? X[0] : X[(k + 1) % MAXV];
-            const double by = wrap ? Y[0] : Y[(k + 1) % MAXV];
-            const double bz = wrap ? Z[0] : Z[(k + 1) % MAXV];
-            const double nx = Y[k] * bz - Z[k] * by;
-            const double ny = Z[k] * bx - X[k] * bz;
-            const double nz = X[k] * by - Y[k] * bx;
-            if (nx * px + ny * py + nz * pz < 0.0) return false;
-        }
-    }
-    // the reference validates vertex ids in the zTop loop (:776-779); no side
-    // effects happen before it, so checking up front is equivalent
-#pragma unroll
-    for (int k = 0; k < MAXV; ++k)
-        if (k < nv && (c.vid[k] < 0 || c.vid[k] >= V)) return false;
-    double lx = 0, ly = 0, lz = 0;
-#pragma unroll
-    for (int k = 0; k < MAXV; ++k)
-        if (k == nv - 1) { lx = X[k]; ly = Y[k]; lz = Z[k]; }
-    double sum = 0.0;
-    double Anext = tri_area(lx, ly, lz, X[0], Y[0], Z[0], px, py, pz);
+    // one pass over the slot pairs (X[i], X[i+1]) -- (X[nv-1], X[0]) at the wrap -- which are both the
+    // polygon's edges (poly[i-1], poly[i]) for IsInMesh (a conjunction of side-effect-free tests, so the
+    // order of the edges is immaterial) and the arguments of A_i = area(poly[i-1], poly[i], p)
+    // (Interpolation.hpp:137-165: A_0 = area(poly[N-1], poly[0], p), A_{i+1} = area(poly[i], poly[i+1], p));
+    // A_i is kept in w[i] until the weights are formed
+    bool inside = true;
 #pragma unroll
     for (int i = 0; i < MAXV; ++i) {
         if (i < nv) {
-            const double Ai = Anext;
             const bool wrap = (i + 1 >= nv);
-            const double nx = wrap ? X[0] : X[(i + 1) % MAXV];
-            const double ny = wrap ? Y[0] : Y[(i + 1) % MAXV];
-            const double nz = wrap ? Z[0] : Z[(i + 1) % MAXV];
-            Anext = tri_area(X[i], Y[i], Z[i], nx, ny, nz, px, py, pz);
-            w[i] = xdiv(BB[i], (Ai * Anext));
-            sum += w[i];
+            const double bx = wrap ? X[0] : X[(i + 1) % MAXV];
+            const double by = wrap ? Y[0] : Y[(i + 1) % MAXV];
+            const double bz = wrap ? Z[0] : Z[(i + 1) % MAXV];
+            const double nx = Y[i] * bz - Z[i] * by;
+            const double ny = Z[i] * bx - X[i] * bz;
+            const double nz = X[i] * by - Y[i] * bx;
+            inside = inside && !(nx * px + ny * py + nz * pz < 0.0);
+            w[i] = tri_area(X[i], Y[i], Z[i], bx, by, bz, px, py, pz);
         } else {
             w[i] = 0.0;
+        }
+    }
+    if (!inside) return false;
+    // (the reference also range-checks the vertex ids in its zTop loop, :776-779; mops_mesh_create
+    // rejects a mesh with an out-of-range active verticesOnCell entry, so that test always passes)
+    // w_i = B_i / (A_i * A_{i+1}), A_nv = A_0, summed in vertex order
+    const double A0 = w[0];
+    double sum = 0.0;
+#pragma unroll
+    for (int i = 0; i < MAXV; ++i) {
+        if (i < nv) {
+            const double An = (i + 1 >= nv) ? A0 : w[(i + 1) % MAXV];
+            w[i] = xdiv(BB[i], (w[i] * An));
+            sum += w[i];
         }
     }
     const double recp = xdiv(1.0, sum);
