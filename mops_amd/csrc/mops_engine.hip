@@ -330,7 +330,7 @@ __device__ __forceinline__ bool weights(const Cell<MAXV>& c, int L, int V, doubl
             const double nx = Y[i] * bz - Z[i] * by;
             const double ny = Z[i] * bx - X[i] * bz;
             const double nz = X[i] * by - Y[i] * bx;
-            inside = inside && !(nx * px + ny * py + nz * pz < 0.0);
+            inside = inside & !(nx * px + ny * py + nz * pz < 0.0);  // no short circuit: straight-line code
             w[i] = tri_area(X[i], Y[i], Z[i], bx, by, bz, px, py, pz);
         } else {
             w[i] = 0.0;
@@ -634,7 +634,7 @@ __device__ __forceinline__ bool weights_finite(const Cell<MAXV>& c, const double
     bool ok = true;
 #pragma unroll
     for (int i = 0; i < MAXV; ++i)
-        if (i < c.nv) ok = ok && isfinite(w[i]);
+        if (i < c.nv) ok = ok & isfinite(w[i]);
     return ok;
 }
 
@@ -667,7 +667,8 @@ __device__ __forceinline__ void pair_sums(const Cell<MAXV>& c, const double* w, 
                                           int k, Pair& S) {
     S.zm = S.zk = S.wm = S.wk = 0.0;
     S.um0 = S.um1 = S.um2 = S.uk0 = S.uk1 = S.uk2 = 0.0;
-    const int64_t zrec = (int64_t)c.V * (L - 1);
+    // 32-bit record indices: V * L < 2^31 (mops_mesh_create), so v*(L-1) + k - 1 fits
+    const uint32_t zrec = (uint32_t)c.V * (uint32_t)(L - 1);
 #pragma unroll
     for (int v0 = 0; v0 < MAXV; v0 += GR) {
         if (v0 < c.nv) {
@@ -677,11 +678,11 @@ __device__ __forceinline__ void pair_sums(const Cell<MAXV>& c, const double* w, 
                 const int v = v0 + j;
                 if (v >= MAXV) break;
     #if defined(MOPS_ABL_PAIR1)
-            const int64_t ri = (int64_t)c.vid[0] * (L - 1) + (k - 1);
+            const uint32_t ri = (uint32_t)c.vid[0] * (uint32_t)(L - 1) + (uint32_t)(k - 1);
 #else
-            const int64_t ri = (v < c.nv) ? (int64_t)c.vid[v] * (L - 1) + (k - 1) : zrec;
+            const uint32_t ri = (v < c.nv) ? (uint32_t)c.vid[v] * (uint32_t)(L - 1) + (uint32_t)(k - 1) : zrec;
 #endif
-                const double2* r = reinterpret_cast<const double2*>(pr + ri * kPairRec);
+                const double2* r = reinterpret_cast<const double2*>(pr + (uint64_t)ri * kPairRec);
 #pragma unroll
                 for (int q = 0; q < kPairRec / 2; ++q) a[j][q] = r[q];
             }
@@ -1589,6 +1590,8 @@ mops_status mops_mesh_create(const mops_mesh_desc* desc, void* stream, mops_mesh
         return fail(MOPS_ERR_INVALID, "mops_mesh_create: invalid sizes");
     if (maxE > kMaxVertex)
         return fail(MOPS_ERR_UNSUPPORTED, "mops_mesh_create: maxEdges > 20 (reference MAX_VERTEX_NUM)");
+    if (V * (int64_t)L >= INT32_MAX)  // level-pair record indices are 32-bit (dev::pair_sums)
+        return fail(MOPS_ERR_UNSUPPORTED, "mops_mesh_create: nVertices * nVertLevels >= 2^31");
     if (!desc->h_n_edges_on_cell || !desc->h_vertices_on_cell || !desc->h_cells_on_cell || !desc->h_cell_coord ||
         !desc->h_vertex_coord)
         return fail(MOPS_ERR_INVALID, "mops_mesh_create: missing mesh array");
