@@ -208,6 +208,7 @@ struct Cell {
     double cx, cy, cz;  // "stay" anchor: the cell centre, or the position of the last walk that kept the cell
     double rs2;         // squared stay radius around the anchor (see dev::walk)
     int vid[MAXV];
+    int vlast;          // vid[nv-1]: slot 0 of the rotated polygon
     int V;              // vertex count (index of the all-zero level-pair record is V*(L-1))
     bool rc;            // compile-time constant per kernel (load_cell<MAXV, RC>): which members below are live
     // polygon positions in "rotated" order: x[0] = poly[nv-1], x[j] = poly[j-1] (1 <= j < nv), so
@@ -244,6 +245,10 @@ __device__ __forceinline__ void load_cell(Cell<MAXV>& c, int cell, const int* __
     c.rc = RC;
 #pragma unroll
     for (int k = 0; k < MAXV; ++k) c.vid[k] = buf[1 + k];
+    c.vlast = 0;
+#pragma unroll
+    for (int k = 0; k < MAXV; ++k)
+        if (k == nv - 1) c.vlast = c.vid[k];
     if constexpr (RC) {
         double px[MAXV], py[MAXV], pz[MAXV];  // natural order
 #pragma unroll
@@ -294,19 +299,13 @@ __device__ __forceinline__ bool weights(const Cell<MAXV>& c, int L, int V, doubl
     if (!isfinite(px) || !isfinite(py) || !isfinite(pz)) return false;
     // rotated slots (see Cell): X[0] = poly[nv-1], X[j] = poly[j-1]
     double X[MAXV], Y[MAXV], Z[MAXV], BB[MAXV];
-    int vlast = 0;  // non-cached polygon: vertex id of poly[nv-1]
-    if (!c.rc) {
-#pragma unroll
-        for (int k = 0; k < MAXV; ++k)
-            if (k == nv - 1) vlast = c.vid[k];
-    }
 #pragma unroll
     for (int j = 0; j < MAXV; ++j) {
         if (c.rc) {
             X[j] = c.x[j]; Y[j] = c.y[j]; Z[j] = c.z[j]; BB[j] = c.B[j];
         } else {
             if (j < nv) {
-                const double4 q = c.vxyz[j == 0 ? vlast : c.vid[(j + MAXV - 1) % MAXV]];
+                const double4 q = c.vxyz[j == 0 ? c.vlast : c.vid[(j + MAXV - 1) % MAXV]];
                 X[j] = q.x; Y[j] = q.y; Z[j] = q.z;
                 BB[j] = c.cellB[(int64_t)c.id * MAXV + j];
             } else {
