@@ -293,3 +293,74 @@ def test_wide_stencil_instantiations(gpu, engine_lib, oracle_lib, max_edges):
                                  euler=(method == 1), cells=got["cells"])
             assert_lines_match(got, ref, f"maxEdges={max_edges} path={back is not None} method={method}")
             assert np.array_equal(got["points"], ref["points"])
+
+
+def test_edge_case_seeds(dev_small, ref_small, small_case, oracle_lib):
+    """Edge cases the reference meets in practice, mixed into ordinary waves:
+    seeds over culled land (nearest cell is coastal, IsInMesh fails: death at
+    step 0), non-finite seeds (no cell, MPASOVisualizerKernels.cpp:744-753 guard),
+    the origin (a chained dead particle's lastPoint, Q1), seeds exactly on cell
+    centres and exactly on mesh vertices (equidistant from three centres: the
+    argmin tie and the IsInMesh boundary), and seed depths above the surface,
+    at 0 and below the bottom (Q5 clamp, bracket end cases)."""
+    from mops_amd import synth
+    from mops_amd.engine import TrajectoryConfig, run_trajectories
+    mesh, _, _ = small_case
+    dm, f0, f1 = dev_small
+    r0, r1 = ref_small
+    land = synth.latlon_to_xyz(np.array([45.0, 47.0, 10.0, 12.0, -25.0, -85.0]),
+                               np.array([-100.0, -98.0, 20.0, 22.0, 135.0, 10.0]))
+    bad = np.array([[np.nan, 0.0, 0.0], [0.0, np.inf, 1.0], [0.0, 0.0, 0.0]])
+    scale = synth.SEED_RADIUS / np.linalg.norm(mesh.cellCoord[0])
+    centres = mesh.cellCoord[::97][:24] * scale
+    verts = mesh.vertexCoord[::131][:24] * scale
+    ocean = synth.uniform_band_seeds(64, seed=77)
+    seeds = np.concatenate([ocean[:20], land, bad, centres, ocean[20:40], verts, ocean[40:]])
+    rng = np.random.default_rng(3)
+    depths = rng.uniform(10.0, 3000.0, len(seeds)).astype(np.float32)
+    depths[::7] = -10.0
+    depths[1::7] = 0.0
+    depths[2::7] = 1.0e6
+    for back, rb in ((None, None), (f1, r1)):
+        for method in (1, 0):
+            cfg = TrajectoryConfig(deltaT=120, simulationDuration=21600, recordT=1800, depth=0.0, method=method)
+            got = run_trajectories(dm, f0, back, cfg, seeds, depths=depths)
+            ref = oracle_lib.run(mesh, r0, rb, seeds, depths=depths, delta_t=120, duration=21600, record_t=1800,
+                                 euler=(method == 1), cells=got["cells"])
+            label = f"edge seeds path={back is not None} method={method}"
+            assert_lines_match(got, ref, label)
+            assert np.array_equal(got["points"], ref["points"], equal_nan=True), label
+            n_ocean, n_land = 20, len(land)
+            # land seeds die before they move; non-finite seeds have no cell
+            assert np.all(got["death_step"][n_ocean:n_ocean + n_land] == 0), label
+            assert np.all(got["cells"][n_ocean + n_land:n_ocean + n_land + 2] == -1), label
+    # seed cells: on-centre seeds locate to that centre (as the oracle's exact 1-NN);
+    # on-vertex seeds to one of the tied nearest centres
+    n0 = 20 + len(land) + len(bad)
+    assert np.array_equal(got["cells"][n0:n0 + len(centres)], oracle_lib.knn(mesh, centres))
+    nv0 = n0 + len(centres) + 20
+    for q, c in zip(verts, got["cells"][nv0:nv0 + len(verts)]):
+        d2 = np.sum((mesh.cellCoord - q) ** 2, axis=1)
+        assert c >= 0 and d2[c] <= d2.min() * (1.0 + 1e-12)
+
+
+def test_empty_and_single_particle(dev_small, ref_small, small_case, oracle_lib):
+    """N = 0 returns empty lines without a launch (MPASOVisualizerKernels.cpp:663-665);
+    N = 1 is one partially filled wave."""
+    from mops_amd import synth
+    from mops_amd.engine import TrajectoryConfig, run_trajectories
+    mesh, _, _ = small_case
+    dm, f0, f1 = dev_small
+    r0, r1 = ref_small
+    cfg = TrajectoryConfig(deltaT=120, simulationDuration=7200, recordT=600, depth=300.0)
+    for back in (None, f1):
+        got = run_trajectories(dm, f0, back, cfg, np.zeros((0, 3)))
+        assert got["points"].shape == (0, cfg.n_records + 1, 3)
+        assert got["death_step"].shape == (0,)
+    seed = synth.uniform_band_seeds(1, seed=5)
+    for back, rb in ((None, None), (f1, r1)):
+        got = run_trajectories(dm, f0, back, cfg, seed)
+        ref = oracle_lib.run(mesh, r0, rb, seed, depth=300.0, delta_t=120, duration=7200, record_t=600,
+                             cells=got["cells"])
+        assert_lines_match(got, ref, f"single particle path={back is not None}")
+        assert np.array_equal(got["points"], ref["points"])
