@@ -111,21 +111,69 @@ def make_gaussian_seeds(n: int, rank: int) -> np.ndarray:
     return np.concatenate(out)[:n]
 
 
-def measured_traffic(key: str, avg_kernel_s: float):
-    """Per-launch DRAM bytes from the committed PMC summary (tools/make_traffic.py), if it is for this workload."""
+def engine_build_id() -> str:
+    """Identity of the trajectory kernel build: sha256 of the engine source and its hipcc flags
+    (tools/make_traffic.py stamps every PMC entry with it, so a changed kernel never inherits
+    another build's measured traffic)."""
+    import hashlib
+    import __graft_entry__ as g
+    h = hashlib.sha256(open(g.HIP_SRC, "rb").read())
+    h.update(" ".join(g.HIPCC_FLAGS[:-1]).encode())  # the -I path differs between machines
+    return h.hexdigest()[:16]
+
+
+def measured_traffic(key: str):
+    """Per-launch DRAM bytes of this workload from profiles/pmc_traffic.json (rocprofv3 FETCH_SIZE/WRITE_SIZE
+    passes merged by tools/make_traffic.py), only if they were measured on this kernel build.
+    Returns (bytes or None, provenance string)."""
     pmc_path = os.path.join(ROOT, "profiles", "pmc_traffic.json")
     if not os.path.exists(pmc_path):
-        return None, None
+        return None, "no profiles/pmc_traffic.json"
     try:
         pm = json.load(open(pmc_path))
-        entries = pm if isinstance(pm, list) else [pm]
-        for e in entries:
-            if e.get("workload") == key:
-                t = e.get("bytes_per_launch")
-                return t, t / avg_kernel_s / 1e9
-    except Exception:
-        pass
-    return None, None
+    except (OSError, ValueError) as e:
+        return None, f"unreadable profiles/pmc_traffic.json: {e}"
+    bid = engine_build_id()
+    for e in (pm if isinstance(pm, list) else [pm]):
+        if e.get("workload") != key:
+            continue
+        if e.get("engine_build") != bid:
+            return None, f"stale: the PMC entry for {key} was measured on engine build {e.get('engine_build')}, not {bid}"
+        return float(e["bytes_per_launch"]), (f"profiles/pmc_traffic.json[{key}] (rocprofv3 2*FETCH_SIZE + WRITE_SIZE "
+                                               f"per launch, engine build {bid}, {e.get('profile', '?')})")
+    return None, f"no PMC entry for {key}"
+
+
+def roofline_block(kernel: str, avg_kernel_s: float, psteps_per_launch: float, B: float, traffic_key: str) -> dict:
+    """The bench line's roofline: HBM GB/s MEASURED by rocprofv3 PMC counters (per launch) over the
+    kernel's HIP-event launch time, against the 8 TB/s peak.  The SURVEY 8(d) bytes model is reported
+    beside it, not as the roofline: it charges a full zTop column and no cross-particle reuse, so its
+    rate exceeds the HBM peak -- the kernel is bound by gather latency and FP64 issue, not by DRAM."""
+    traffic, src = measured_traffic(traffic_key)
+    achieved = traffic / avg_kernel_s / 1e9 if traffic is not None else None
+    alg = B * psteps_per_launch / avg_kernel_s / 1e9
+    return {
+        "bound": "hbm",
+        "achieved": achieved,
+        "peak": PEAK_HBM_GBS,
+        "unit": "GB/s",
+        "frac": (achieved / PEAK_HBM_GBS) if achieved is not None else None,
+        "traffic": traffic,
+        "traffic_source": src,
+        "limiter": ("not DRAM: dependent per-lane gathers (L1/TA-served) and FP64 VALU issue at 3 waves/SIMD "
+                    "(DESIGN.md section 3)"),
+        "kernel": kernel,
+        "particle_steps_per_launch": psteps_per_launch,
+        "avg_launch_ms": avg_kernel_s * 1e3,
+        "algorithmic_model": {
+            "bytes_per_particle_step": B,
+            "gbs": alg,
+            "source": "SURVEY.md 8(d): one compulsory stencil fetch per particle-step, full zTop column (8*nv*L)",
+            "note": ("a model of what a reuse-free implementation would fetch; the engine reads one level-pair "
+                     "record per vertex and lanes share stencils through L1/L2, so this rate is not a DRAM rate "
+                     "and may exceed the HBM peak"),
+        },
+    }
 
 
 def algorithmic_bytes_per_pstep(nv: float, L: int, S: int = 1) -> float:
@@ -206,9 +254,12 @@ def main():
     segments = [(bounds[i], bounds[i + 1]) for i in range(len(bounds) - 1)]
     compute = torch.cuda.Stream(dev)
     comm = torch.cuda.Stream(dev)
-    gathered = None
+    gathered = gathered_ids = None
     if world > 1:
+        # records are gathered in each rank's slot (locality) order, with the rank's slot -> particle
+        # ids once per call, so the gathered slabs map back to particles (distributed.unshard_slots)
         gathered = torch.empty((ps.K, world, 6, n), dtype=torch.float64, device=dev)
+        gathered_ids = torch.empty((world, n), dtype=torch.int32, device=dev)
     seeds_dev = ps.seeds
 
     kernel_ms = []
@@ -219,6 +270,12 @@ def main():
             ps.reset(depth=args.depth)
             dmesh.locate(seeds_dev.data_ptr(), ps.cell.data_ptr(), n, stream=compute)
             ps.reorder(stream=compute)
+            if world > 1:
+                sorted_ev = torch.cuda.Event()
+                sorted_ev.record(compute)
+                comm.wait_event(sorted_ev)
+                with torch.cuda.stream(comm):
+                    all_gather_flat(dist, gathered_ids.view(-1), ps.ids, args.backend)
             for (s0, s1) in segments:
                 if timed:
                     e0 = torch.cuda.Event(enable_timing=True); e1 = torch.cuda.Event(enable_timing=True)
@@ -273,9 +330,9 @@ def main():
     nv_mean = float(np.mean(mesh.nEdgesOnCell.astype(np.float64)))
     B = algorithmic_bytes_per_pstep(nv_mean, mesh.nVertLevels, 2 if pathline else 1)
     psteps_per_launch = attempted / len(segments)
-    achieved = B * psteps_per_launch / avg_kernel_s / 1e9
-    traffic, measured = measured_traffic(f"ec30to60_{args.mode}_{args.method}_{args.particles}_seg{seg}",
-                                         avg_kernel_s)
+    roof = roofline_block(f"traj_kernel<7,{str(pathline).lower()},{str(args.method == 'euler').lower()}> "
+                          f"({args.mode} {args.method})", avg_kernel_s, psteps_per_launch, B,
+                          f"ec30to60_{args.mode}_{args.method}_{args.particles}_seg{seg}")
 
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
@@ -314,23 +371,7 @@ def main():
             "nominal_particle_steps_per_call": n_all * n_steps,
             "attempted_particle_steps_per_call": attempted_all,
             "dead_fraction": dead_all / max(n_all, 1),
-            "roofline": {
-                "bound": "hbm",
-                "achieved": achieved,
-                "peak": PEAK_HBM_GBS,
-                "unit": "GB/s",
-                "frac": achieved / PEAK_HBM_GBS,
-                "traffic": traffic,
-                "kernel": f"traj_kernel<7,{str(pathline).lower()},{str(args.method == 'euler').lower()}> "
-                          f"({args.mode} {args.method})",
-                "algorithmic_bytes_per_particle_step": B,
-                "algorithmic_bytes_note": ("SURVEY.md 8(d) model: full zTop column (8*nv*L) per step; the engine "
-                                           "reads ~2 levels per step, so frac > 1 is possible -- see measured_*"),
-                "measured_hbm_gbs": measured,
-                "measured_frac": (measured / PEAK_HBM_GBS) if measured else None,
-                "particle_steps_per_launch": psteps_per_launch,
-                "avg_launch_ms": avg_kernel_s * 1e3,
-            },
+            "roofline": roof,
             "cpu_baseline": cpu,
         }
         print(json.dumps(line))
@@ -442,13 +483,12 @@ def main_chain(args, mesh, dev, world, rank):
     B = algorithmic_bytes_per_pstep(nv_mean, mesh.nVertLevels, 2)
     launches_per_call = len(timing) / args.steps
     psteps_per_launch = attempted / args.steps / launches_per_call
-    achieved = B * psteps_per_launch / avg_kernel_s / 1e9
     mesh_class = "EC30to60" if args.config == 3 else "oRRS18to6"
     from mops_amd.chain import REORDER_SECONDS
     seg_key = args.segment if args.segment > 0 else min(args.duration // args.dt, REORDER_SECONDS // args.dt)
-    traffic, measured = measured_traffic(f"{mesh_class.lower()}_chain{args.config}_{args.method}_{args.particles}"
-                                         f"_seg{seg_key}",
-                                         avg_kernel_s)
+    roof = roofline_block(f"traj_kernel<7,true,{str(args.method == 'euler').lower()}> (pathline {args.method})",
+                          avg_kernel_s, psteps_per_launch, B,
+                          f"{mesh_class.lower()}_chain{args.config}_{args.method}_{args.particles}_seg{seg_key}")
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         seed_cells = dmesh_locate_host(dmesh, seeds, dev)
@@ -484,15 +524,7 @@ def main_chain(args, mesh, dev, world, rank):
                                   "per pair") if world > 1 else "none"},
             "nominal_particle_steps_per_call": n_all * n_steps,
             "attempted_particle_steps_per_call": attempted_all / args.steps,
-            "roofline": {
-                "bound": "hbm", "achieved": achieved, "peak": PEAK_HBM_GBS, "unit": "GB/s",
-                "frac": achieved / PEAK_HBM_GBS, "traffic": traffic,
-                "kernel": f"traj_kernel<7,true,{str(args.method == 'euler').lower()}> (pathline {args.method})",
-                "algorithmic_bytes_per_particle_step": B,
-                "algorithmic_bytes_note": "SURVEY.md 8(d) model (S=2); see measured_* for DRAM traffic",
-                "measured_hbm_gbs": measured,
-                "measured_frac": (measured / PEAK_HBM_GBS) if measured else None,
-                "particle_steps_per_launch": psteps_per_launch, "avg_launch_ms": avg_kernel_s * 1e3},
+            "roofline": roof,
             "cpu_baseline": cpu,
         }))
     if world > 1:

@@ -136,5 +136,6 @@ int main(int argc, char** argv) {
     std::printf("lines %zu %zu points %zu lattice %zu\n", stream.size(), path.size(),
                 stream.empty() ? (size_t)0 : stream[0].points.size(), lattice.size());
     MOPS_PrintTimingSummary();
+    MOPS_Finalize();
     return 0;
 }

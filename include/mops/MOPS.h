@@ -167,6 +167,10 @@ void MOPS_ActiveAttribute(int t1, std::optional<int> t2 = std::nullopt);
 std::vector<TrajectoryLine> MOPS_RunStreamLine(TrajectorySettings* config, std::vector<CartesianCoord>& sample_points);
 std::vector<TrajectoryLine> MOPS_RunPathLine(TrajectorySettings* config, std::vector<CartesianCoord>& sample_points);
 void MOPS_GenerateSamplePoints(SamplingSettings* config, std::vector<CartesianCoord>& sample_points);
+// Extension (the reference has no teardown): releases the mesh and fields held in HBM by the
+// global app.  Call it before the HIP runtime shuts down; nothing is freed from a static
+// destructor at exit.
+void MOPS_Finalize();
 
 void MOPS_ResetTiming();
 void MOPS_PrintTimingSummary();

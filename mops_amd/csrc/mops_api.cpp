@@ -68,7 +68,11 @@ struct App {
         mesh = nullptr;
         front = back = nullptr;
     }
-    ~App() { release(); }
+    // No device frees here: g_app is destroyed during static destruction, when the
+    // HIP runtime may already be torn down.  Device state is released by MOPS_Init
+    // (re-initialisation) and MOPS_Finalize; whatever is left at exit is reclaimed
+    // with the process.
+    ~App() = default;
 };
 App g_app;
 
@@ -242,6 +246,12 @@ void MOPS_Init(const char* device) {
         std::cout << " [ system information ]\nDevice selected : " << prop.name << " (" << prop.gcnArchName
                   << ", HIP engine)\n";
     g_app.grid = std::make_shared<MPASOGrid>();
+}
+
+void MOPS_Finalize() {
+    g_app.release();
+    g_app.sols.clear();
+    g_app.state = State::Idle;
 }
 
 void MOPS_Begin() { g_app.state = State::Configuring; }

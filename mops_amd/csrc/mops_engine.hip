@@ -100,8 +100,13 @@ struct mops_field {
     double* d_zt = nullptr;   // cellVertexZTop [V][L]
     double* d_vel = nullptr;  // cellVertexVelocity [V][L][3]
     double* d_w = nullptr;    // cellVertexVertVelocity [V][L+1]
-    uint8_t* d_mono = nullptr;  // [C] 1 = every vertex column of the cell strictly decreasing (margin)
-    uint8_t* d_vmono = nullptr;  // [V] the same test per vertex column (mono_kernel's first pass)
+    // [C] fast-path word (mono_kernel, read by dev::fast_ok): bit 31 = eligible, bits 20..26 = km,
+    // the cell's decreasing prefix (every non-zero vertex column drops by >= 1e-6 m per level over
+    // levels 0..km), bits 0..19 = which polygon slots are identically-zero columns (boundary
+    // vertices, quirk Q10)
+    uint32_t* d_mono = nullptr;
+    int32_t* d_vmono = nullptr;  // [V] first level that breaks the vertex column's decrease (L = none)
+    uint8_t* d_vzero = nullptr;  // [V] 1 = every level of the vertex column is 0 (boundary vertex)
     // level-pair records [V][L-1][kPairRec] doubles, record k-1 of vertex v =
     // {z_{k-1}, z_k, w_{k-1}, w_k, vel_{k-1} (3), vel_k (3)}: one 80-B,
     // 16-B-aligned read (5 x dwordx4) gives a vertex's whole contribution when
@@ -118,6 +123,25 @@ struct mops_field {
 // device helpers -- every expression keeps the reference's evaluation order
 // ===========================================================================
 namespace dev {
+
+#if defined(MOPS_WAVE_STAMPS)
+// Diagnostic builds only (tools/build_variant.sh -DMOPS_WAVE_STAMPS): 8 words per
+// slot -- {start, end} in s_memrealtime ticks (100 MHz), the raw HW_ID / XCC_ID
+// registers, then event counts: walks, cell loads after step 0, evaluations that
+// missed the hinted fast bracket, zTop levels read by the brackets (low 32 bits)
+// + bracket_scan calls (high 32).  Set with mops_debug_stamps; never in a product build.
+__device__ unsigned long long* g_stamps;
+__device__ long long g_stamps_cap;
+__device__ __forceinline__ unsigned long long* stamp_slot() {
+    const unsigned nblk = gridDim.x, b = blockIdx.x, xcd = b % 8u, q = nblk / 8u, r = nblk % 8u;
+    const unsigned blk = (xcd < r ? xcd * (q + 1u) : r * (q + 1u) + (xcd - r) * q) + b / 8u;
+    const long long slot = (long long)blk * blockDim.x + threadIdx.x;
+    return (g_stamps && slot < g_stamps_cap) ? g_stamps + 8 * slot : nullptr;
+}
+#define MOPS_CNT(i, v) do { unsigned long long* _p = dev::stamp_slot(); if (_p) _p[i] += (v); } while (0)
+#else
+#define MOPS_CNT(i, v) do { } while (0)
+#endif
 
 // Ablation hooks for perf experiments only (tools/build_variant.sh -DMOPS_ABL_*):
 // they break parity and are never set in a product build.
@@ -204,7 +228,7 @@ template <int MAXV>
 struct Cell {
     int id;
     int nv;
-    bool mono0, mono1;  // fast-path flags of the cell for the front / back field
+    uint32_t mono0, mono1;  // fast-path words of the cell for the front / back field (mops_field::d_mono)
     double cx, cy, cz;  // "stay" anchor: the cell centre, or the position of the last walk that kept the cell
     double rs2;         // squared stay radius around the anchor (see dev::walk)
     int vid[MAXV];
@@ -222,11 +246,11 @@ struct Cell {
 
 template <int MAXV, bool RC>
 __device__ __forceinline__ void load_cell(Cell<MAXV>& c, int cell, const int* __restrict__ cellrec,
-                                          const double4* __restrict__ vxyz, const uint8_t* __restrict__ mono0,
-                                          const uint8_t* __restrict__ mono1, const double4* __restrict__ cxyz,
+                                          const double4* __restrict__ vxyz, const uint32_t* __restrict__ mono0,
+                                          const uint32_t* __restrict__ mono1, const double4* __restrict__ cxyz,
                                           const double* __restrict__ cellB) {
-    c.mono0 = mono0[cell] != 0;
-    c.mono1 = mono1[cell] != 0;
+    c.mono0 = mono0[cell];
+    c.mono1 = mono1[cell];
     {
         const double4 q = cxyz[cell];
         c.cx = q.x; c.cy = q.y; c.cz = q.z; c.rs2 = q.w;
@@ -360,6 +384,7 @@ __device__ __forceinline__ bool weights(const Cell<MAXV>& c, int L, int V, doubl
 template <int MAXV>
 __device__ __forceinline__ double col(const Cell<MAXV>& c, const double* w, const double* __restrict__ zt, int L,
                                       int k) {
+    MOPS_CNT(7, 1);
     double acc = 0.0;
 #pragma unroll
     for (int v = 0; v < MAXV; ++v)
@@ -384,6 +409,7 @@ __device__ __forceinline__ int bracket_scan(const Cell<MAXV>& c, const double* w
     const double eps = 1e-8;
     const double z0 = col<MAXV>(c, w, zt, L, 0);
     double z1 = col<MAXV>(c, w, zt, L, 1);
+    MOPS_CNT(7, 1ull << 32);
     if (z1 > z0) z1 = z0 - 1e-9;
     if (d > z0 + eps) {  // above the surface (PATH: reference layer 0 reads z[-1])
         zdn = z1; zup = z0;
@@ -441,21 +467,23 @@ __device__ __forceinline__ int bracket_scan(const Cell<MAXV>& c, const double* w
     return layer;
 }
 
-// Fast, exact bracket for cells whose vertex columns are all strictly
-// decreasing by >= 1e-6 m (field flag d_mono) when every Wachspress weight is
-// finite.  The weights are then >= 0 (triangle areas are sqrt's) and sum to
-// 1 +- nv ulp, so the interpolated column is strictly decreasing with a margin
-// far above its rounding error (|z| <= 1e6 m: error < 1e-9): the
-// reference's fix-up never fires and z'_k = z_k, computable level by level.
-// a and b (see bracket_scan) are then found by walking from the particle's
-// previous layer (`hint`); typically two levels plus the surface level are
-// read instead of the whole column.  Any hint gives the same result.
+// Fast, exact bracket for a particle whose interpolated column is provably
+// strictly decreasing over its first km + 1 levels (fast_ok: km = the cell's
+// decreasing prefix, every non-zero vertex column drops by >= 1e-6 m per
+// level there): the reference's fix-up never fires on levels 1..km, so z'_k
+// = z_k there, computable level by level, and the bracket predicates are
+// monotone in the level everywhere (the fixed column is non-increasing by
+// construction).  a and b (see bracket_scan) are then found by walking from
+// the particle's previous layer (`hint`); typically two levels plus the
+// surface level are read instead of the whole column.  Any hint gives the
+// same result.  A walk that would need a level below km returns -2 (the
+// caller runs bracket_scan): below the prefix the fix-up may have fired.
 template <int MAXV, bool PATH>
 __device__ __forceinline__ int bracket_mono(const Cell<MAXV>& c, const double* w, const double* __restrict__ zt,
-                                            int L, double d, int& hint, double& zdn, double& zup) {
+                                            int L, int km, double d, int& hint, double& zdn, double& zup) {
     const double eps = 1e-8;
     int h = hint;
-    const bool hint_ok = (h >= 1 && h <= L - 1);
+    const bool hint_ok = (h >= 1 && h <= km);
     if (!hint_ok) h = 1;
     // one batch of independent loads: z_0, z_{h-1}, z_h (per-level sums keep
     // the reference's vertex order)
@@ -475,12 +503,13 @@ __device__ __forceinline__ int bracket_mono(const Cell<MAXV>& c, const double* w
         zup = z0; hint = 1;
         return 1;
     }
-    if (!hint_ok) {  // no hint: lower_bound of Q over [1, L-1] by bisection
-        int lo = 1, hi = L;
+    if (!hint_ok) {  // no hint: lower_bound of Q over [1, km] by bisection
+        int lo = 1, hi = km + 1;
         while (lo < hi) {
             const int mid = (lo + hi) >> 1;
             if (d >= col<MAXV>(c, w, zt, L, mid) - eps) hi = mid; else lo = mid + 1;
         }
+        if (lo > km && km < L - 1) return -2;  // a lies below the prefix
         h = (lo <= L - 1) ? lo : L - 1;
         zh = col<MAXV>(c, w, zt, L, h);
         zhm1 = (h == 1) ? z0 : col<MAXV>(c, w, zt, L, h - 1);
@@ -502,12 +531,13 @@ __device__ __forceinline__ int bracket_mono(const Cell<MAXV>& c, const double* w
         double zk = zh, zprev = zh;
         bool found = false;
         while (k < L - 1) {
+            if (k >= km) return -2;
             ++k;
             zprev = zk;
             zk = col<MAXV>(c, w, zt, L, k);
             if (d >= zk - eps) { found = true; break; }
         }
-        if (!found) {  // Q(L-1) false  <=>  d < z_{L-1} - eps: the "below the bottom" branch
+        if (!found) {  // Q(L-1) false  <=>  d < z_{L-1} - eps: the "below the bottom" branch (km = L-1 here)
             const double zlm1 = (k == h) ? zhm1 : zprev;
             zdn = zk; zup = zlm1; hint = L - 1;
             return L - 1;
@@ -519,6 +549,7 @@ __device__ __forceinline__ int bracket_mono(const Cell<MAXV>& c, const double* w
     int b = a;
     double zb = za, zbm1 = zam1;
     while (b < L - 1 && d <= zb + eps) {
+        if (b >= km) return -2;
         const double zn = col<MAXV>(c, w, zt, L, b + 1);
         zbm1 = zb; zb = zn; ++b;
     }
@@ -573,6 +604,7 @@ __device__ unsigned long long g_prof[8];
 template <int MAXV>
 __device__ __forceinline__ int walk(Cell<MAXV>& c, int cell, double x, double y, double z,
                                     const int* __restrict__ cellrec, const double4* __restrict__ cxyz, int C) {
+    MOPS_CNT(4, 1);
     constexpr int REC = ((1 + 2 * MAXV) + 3) / 4 * 4;
     constexpr int Q0 = (1 + MAXV) / 4, Q1 = (2 * MAXV) / 4;  // int4 words holding cellsOnCell
     int buf[(Q1 - Q0 + 1) * 4];
@@ -637,6 +669,36 @@ __device__ __forceinline__ bool weights_finite(const Cell<MAXV>& c, const double
     return ok;
 }
 
+// May the hinted fast bracket (layer_eval / bracket_mono) run for this cell,
+// field and particle, and over which levels?  `m` is the field's fast-path
+// word for the cell (mono_kernel): every vertex column is either identically
+// 0 (a boundary vertex, quirk Q10) or strictly decreasing by >= 1e-6 m per
+// level over levels 0..km ("decreasing" vertices, at least one).  Returns km,
+// or -1 for "general bracket only".
+//
+// Why km is exact: with finite weights w_v >= 0 (triangle areas are sqrt's),
+// a zero column adds w_v * 0 = +0 to each level sum, i.e. nothing, so the
+// computed z_k is the rounded sum over the decreasing vertices only.  Its
+// rounding error is below 21 * 2^-53 * sum_dec(w_v |z_v,k|) <= 2.4e-15 * W *
+// 1e6 m (|z| <= 1e6 m, <= 20 terms, W = sum of the decreasing vertices'
+// weights), while the exact drop z_{k-1} - z_k is >= W * 1e-6 m.  Both scale
+// with W, so for every W > 0 the computed column strictly decreases over
+// 0..km (drop - 2 * error >= W * (1e-6 - 4.8e-9)); W >= 1e-200 keeps every
+// term clear of subnormal rounding.  The reference's fix-up therefore never
+// fires there and its bracket predicates are monotone in the level.
+template <int MAXV>
+__device__ __forceinline__ int fast_ok(const Cell<MAXV>& c, uint32_t m, bool wfin, const double* w) {
+    if (!(m & 0x80000000u) || !wfin) return -1;
+    const int km = (int)((m >> 20) & 0x7fu);
+    const uint32_t zmask = m & 0x000fffffu;
+    if (zmask == 0u) return km;
+    double W = 0.0;
+#pragma unroll
+    for (int i = 0; i < MAXV; ++i)
+        if (i < c.nv && !((zmask >> i) & 1u)) W += w[i];
+    return (W >= 1e-200) ? km : -1;
+}
+
 struct Field {
     const double* __restrict__ zt;   // cellVertexZTop [V][L]
     const double* __restrict__ pr;   // level-pair records [V][L-1][kPairRec] (see mops_field)
@@ -699,22 +761,24 @@ __device__ __forceinline__ void pair_sums(const Cell<MAXV>& c, const double* w, 
     }
 }
 
-// Layer + values for one field.  Fast path (monotone cell, finite weights,
-// valid hint h): ONE record per vertex decides whether the layer is h --
-// Q(h), !Q(h-1), !P(h+1) (notation of bracket_scan), i.e. a = b = h, which
-// both the binary search (streamline) and the linear scan (pathline) resolve
-// to h -- plus the reference's "above the surface" test d > z_0 + eps first.
-// That test needs no z_0 in the record: for h == 1, z_0 = z_{h-1}; for h >= 2
-// the accepted case has d < z_{h-1} - eps, and in a monotone cell z_{h-1} <=
-// z_1 < z_0 - 1e-6 (margin >> the 1e-9 rounding of the sums), so d > z_0 +
-// eps is false there.  Otherwise the exact general bracket runs and the
-// record of the final layer is read.
+// Layer + values for one field.  Fast path (fast_ok gave the decreasing
+// prefix km >= 1 and the hint h is in 1..km): ONE record per vertex decides
+// whether the layer is h -- Q(h), !Q(h-1), !P(h+1) (notation of
+// bracket_scan), i.e. a = b = h, which both the binary search (streamline)
+// and the linear scan (pathline) resolve to h; the record's z_{h-1}, z_h are
+// the fixed-up z'_{h-1}, z'_h because h <= km -- plus the reference's "above
+// the surface" test d > z_0 + eps first.  That test needs no z_0 in the
+// record: for h == 1, z_0 = z_{h-1}; for h >= 2 the accepted case has d <
+// z_{h-1} - eps < z_0 - eps (strictly decreasing prefix), so d > z_0 + eps is
+// false there.  Otherwise bracket_mono walks from the hint inside the prefix,
+// and bracket_scan (the whole fixed-up column) runs when the walk would leave
+// it; the record of the final layer is then read.
 template <int MAXV, bool PATH, int GR>
-__device__ __forceinline__ int layer_eval(const Cell<MAXV>& c, const double* w, bool mono_ok, const Field& f, int L,
+__device__ __forceinline__ int layer_eval(const Cell<MAXV>& c, const double* w, int km, const Field& f, int L,
                                           double d, int& hint, Pair& S) {
     const double eps = 1e-8;
     const int h = hint;
-    if (mono_ok && h >= 1 && h <= L - 1) {
+    if (h >= 1 && h <= km) {  // km = -1: general bracket only (fast_ok)
         pair_sums<MAXV, GR>(c, w, f.pr, L, h, S);
         bool ok;
         if (h == 1 && d > S.zm + eps) {  // above the surface (z_0 = z_{h-1} here)
@@ -727,11 +791,11 @@ __device__ __forceinline__ int layer_eval(const Cell<MAXV>& c, const double* w, 
         }
         if (ok) return h;
     }
+    MOPS_CNT(6, 1);
     double zdn, zup;
-    int layer;
-    if (mono_ok) {
-        layer = bracket_mono<MAXV, PATH>(c, w, f.zt, L, d, hint, zdn, zup);
-    } else {
+    int layer = -2;
+    if (km >= 1) layer = bracket_mono<MAXV, PATH>(c, w, f.zt, L, km, d, hint, zdn, zup);
+    if (layer == -2) {
         layer = bracket_scan<MAXV, PATH>(c, w, f.zt, L, d, zdn, zup);
         hint = layer;
     }
@@ -750,7 +814,8 @@ __device__ __forceinline__ bool eval_stream(const Cell<MAXV>& c, int L, int V, c
     double w[MAXV];
     if (!weights<MAXV>(c, L, V, px, py, pz, w)) return false;
     Pair S;
-    const int layer = layer_eval<MAXV, false, GR>(c, w, c.mono0 && weights_finite<MAXV>(c, w), f, L, d, hint, S);
+    const int layer = layer_eval<MAXV, false, GR>(c, w, fast_ok<MAXV>(c, c.mono0, weights_finite<MAXV>(c, w), w), f,
+                                                  L, d, hint, S);
     if (layer < 0) return false;
     const double zdn = S.zk, zup = S.zm;
     double x = d;
@@ -779,8 +844,8 @@ __device__ __forceinline__ bool eval_path(const Cell<MAXV>& c, int L, int V, con
     if (!weights<MAXV>(c, L, V, px, py, pz, w)) return false;
     const bool wfin = weights_finite<MAXV>(c, w);
     Pair F, B;
-    const int lf = layer_eval<MAXV, true, GR>(c, w, c.mono0 && wfin, ff, L, d, hint0, F);
-    const int lb = layer_eval<MAXV, true, GR>(c, w, c.mono1 && wfin, fb, L, d, hint1, B);
+    const int lf = layer_eval<MAXV, true, GR>(c, w, fast_ok<MAXV>(c, c.mono0, wfin, w), ff, L, d, hint0, F);
+    const int lb = layer_eval<MAXV, true, GR>(c, w, fast_ok<MAXV>(c, c.mono1, wfin, w), fb, L, d, hint1, B);
     if (lf < 0 || lb < 0) return false;
     const double xf = dmax(F.zk, dmin(d, F.zm));
     const double denf = F.zm - F.zk;
@@ -814,8 +879,8 @@ struct TrajArgs {
     const double4* __restrict__ vxyz;
     int C, V, L;
     dev::Field f0, f1;
-    const uint8_t* __restrict__ mono0;
-    const uint8_t* __restrict__ mono1;
+    const uint32_t* __restrict__ mono0;
+    const uint32_t* __restrict__ mono1;
     const int* __restrict__ order;  // slot -> particle (NULL = identity)
     const double* __restrict__ cellB;  // per-cell Wachspress B_i
     double* px; double* py; double* pz;
@@ -881,6 +946,19 @@ __global__ void __launch_bounds__(kTrajBlock, (TrajWaves<MAXV, PATH, EULER>::val
     const unsigned blk = (xcd < r ? xcd * (q + 1u) : r * (q + 1u) + (xcd - r) * q) + b / 8u;
     const int64_t slot = (int64_t)blk * blockDim.x + threadIdx.x;
     if (slot >= a.n) return;
+#if defined(MOPS_WAVE_STAMPS)
+    unsigned long long* stamp = dev::stamp_slot();
+    if (stamp) {
+        stamp[0] = __builtin_amdgcn_s_memrealtime();
+        stamp[2] = (unsigned)__builtin_amdgcn_s_getreg((31 << 11) | 4);   // HW_ID
+        stamp[3] = (unsigned)__builtin_amdgcn_s_getreg((31 << 11) | 20);  // XCC_ID
+        stamp[1] = stamp[0];
+    }
+    struct StampEnd {
+        unsigned long long* p;
+        __device__ ~StampEnd() { if (p) p[1] = __builtin_amdgcn_s_memrealtime(); }
+    } stamp_end{stamp};
+#endif
     const int64_t pid = a.order ? (int64_t)a.order[slot] : slot;
     if (a.death[pid] >= 0) return;  // the reference's lambda has returned
     double x = a.px[pid], y = a.py[pid], z = a.pz[pid];
@@ -930,6 +1008,7 @@ __global__ void __launch_bounds__(kTrajBlock, (TrajWaves<MAXV, PATH, EULER>::val
 #else
             if (!(ex * ex + ey * ey + ez * ez < c.rs2)) {
                 cell = dev::walk<MAXV>(c, cell, x, y, z, a.cellrec, a.cxyz, C);
+                if (c.id != cell) MOPS_CNT(5, 1);
                 if (c.id != cell) dev::load_cell<MAXV, RCache<MAXV, PATH, EULER>::value>(c, cell, a.cellrec, a.vxyz, a.mono0, a.mono1, a.cxyz, a.cellB);
             }
 #endif
@@ -1363,30 +1442,59 @@ __global__ void locate_radius_kernel(int64_t C, const double4* cxyz, const uint6
 // fast-path flags and particle locality order
 // ===========================================================================
 
-// d_mono[c] = 1 iff every vertex column of cell c is finite, |z| <= 1e6 m and
-// strictly decreasing by >= 1e-6 m per level (see bracket_mono).  Two passes:
-// a per-vertex flag from one coalesced (vertex, level) element per thread
-// (every level's test reads the raw z_{l-1}, exactly as the per-column scan),
-// then a per-cell AND over the polygon's vertices.
-__global__ void vertex_mono_kernel(int64_t V, int L, const double* __restrict__ zt, uint8_t* __restrict__ vflag) {
+// Fast-path word per cell (see dev::fast_ok).  Two passes: per-vertex facts
+// from one coalesced (vertex, level) element per thread -- vfail: the first
+// level l that is non-finite, has |z| > 1e6 m or (l > 0) does not drop below
+// z_{l-1} - 1e-6 m (every level's test reads the raw z_{l-1}, exactly as a
+// per-column scan would; L if none); vzero: every level is 0 -- then a
+// per-cell pass over the polygon's vertices.
+__global__ void fill_i32_kernel(int64_t n, int32_t v, int32_t* __restrict__ p) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n) p[i] = v;
+}
+
+__global__ void vertex_mono_kernel(int64_t V, int L, const double* __restrict__ zt, int32_t* __restrict__ vfail,
+                                   uint8_t* __restrict__ vzero) {
     const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= V * L) return;
     const int l = (int)(i % L);
     const double z = zt[i];
     bool ok = isfinite(z) && fabs(z) <= 1e6;
     if (l > 0) ok = ok && (z < zt[i - 1] - 1e-6);
-    if (!ok) vflag[i / L] = 0;  // every writer stores 0: the race is benign
+    if (!ok) {
+        // only the first level of each failing run competes for the minimum
+        bool prev_ok = true;
+        if (l > 0) {
+            const double zp = zt[i - 1];
+            prev_ok = isfinite(zp) && fabs(zp) <= 1e6;
+            if (l > 1) prev_ok = prev_ok && (zp < zt[i - 2] - 1e-6);
+        }
+        if (l == 0 || prev_ok) atomicMin(&vfail[i / L], l);
+    }
+    if (z != 0.0) vzero[i / L] = 0;  // every writer stores 0: the race is benign
 }
 
-__global__ void mono_kernel(int64_t C, int maxv, int rec_ints, const int* cellrec, const uint8_t* vflag, int L,
-                            uint8_t* mono) {
+__global__ void mono_kernel(int64_t C, int maxv, int rec_ints, const int* cellrec, const int32_t* vfail,
+                            const uint8_t* vzero, int L, uint32_t* mono) {
     const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= C) return;
     const int* r = cellrec + i * rec_ints;
     const int nv = r[0];
     bool ok = (nv >= 1 && nv <= kMaxVertex && L >= 2);
-    for (int k = 0; k < nv && ok; ++k) ok = vflag[r[1 + k]] != 0;
-    mono[i] = ok ? 1 : 0;
+    bool any_dec = false;
+    int km = L - 1;
+    uint32_t zmask = 0u;
+    for (int k = 0; k < nv && ok; ++k) {
+        const int v = r[1 + k];
+        if (vzero[v]) {
+            zmask |= 1u << k;
+        } else {
+            any_dec = true;
+            km = min(km, vfail[v] - 1);  // levels 0..vfail-1 are good
+        }
+    }
+    ok = ok && any_dec && km >= 1;
+    mono[i] = ok ? (0x80000000u | ((uint32_t)km << 20) | zmask) : 0u;
 }
 
 // Wachspress B_i = area(poly[i-1], poly[i], poly[i+1]) per cell, with the
@@ -1539,6 +1647,7 @@ void free_mesh(mops_mesh* m) {
 void free_field(mops_field* f) {
     if (!f) return;
     (void)hipFree(f->d_zt); (void)hipFree(f->d_vel); (void)hipFree(f->d_w); (void)hipFree(f->d_mono); (void)hipFree(f->d_vmono);
+    (void)hipFree(f->d_vzero);
     (void)hipFree(f->d_pr);
     (void)hipFree(f->d_ztc); (void)hipFree(f->d_velc);
     delete f;
@@ -1575,6 +1684,21 @@ int mops_debug_prof(uint64_t* out) {
     for (int i = 0; i < 8; ++i) out[i] = h[i];
     const unsigned long long z[8] = {0, 0, 0, 0, 0, 0, 0, 0};
     if (hipMemcpyToSymbol(HIP_SYMBOL(dev::g_prof), z, sizeof(z)) != hipSuccess) return -1;
+    return 0;
+}
+#endif
+#if defined(MOPS_WAVE_STAMPS)
+// diagnostic builds only: per-slot stamps buffer (device, 4 x u64 per slot) and the
+// occupancy API's resident 64-thread blocks per CU of the four MAXV=7 trajectory kernels
+int mops_debug_stamps(unsigned long long* d_buf, long long cap, int* occ) {
+    if (hipMemcpyToSymbol(HIP_SYMBOL(dev::g_stamps), &d_buf, sizeof(d_buf)) != hipSuccess) return -1;
+    if (hipMemcpyToSymbol(HIP_SYMBOL(dev::g_stamps_cap), &cap, sizeof(cap)) != hipSuccess) return -1;
+    if (occ) {
+        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ[0], traj_kernel<7, false, true>, kTrajBlock, 0) != hipSuccess) return -1;
+        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ[1], traj_kernel<7, false, false>, kTrajBlock, 0) != hipSuccess) return -1;
+        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ[2], traj_kernel<7, true, true>, kTrajBlock, 0) != hipSuccess) return -1;
+        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ[3], traj_kernel<7, true, false>, kTrajBlock, 0) != hipSuccess) return -1;
+    }
     return 0;
 }
 #endif
@@ -1751,10 +1875,13 @@ static mops_status compute_mono(const mops_mesh* mesh, mops_field* f, hipStream_
     }
     if (!f->d_mono) MOPS_TRY(dmalloc(&f->d_mono, (size_t)mesh->C, &f->bytes));
     if (!f->d_vmono) MOPS_TRY(dmalloc(&f->d_vmono, (size_t)mesh->V, &f->bytes));
-    HIP_TRY(hipMemsetAsync(f->d_vmono, 1, (size_t)mesh->V, s));
-    vertex_mono_kernel<<<grid_for(mesh->V * mesh->L), kBlock, 0, s>>>(mesh->V, mesh->L, f->d_zt, f->d_vmono);
+    if (!f->d_vzero) MOPS_TRY(dmalloc(&f->d_vzero, (size_t)mesh->V, &f->bytes));
+    fill_i32_kernel<<<grid_for(mesh->V), kBlock, 0, s>>>(mesh->V, mesh->L, f->d_vmono);
+    HIP_TRY(hipMemsetAsync(f->d_vzero, 1, (size_t)mesh->V, s));
+    vertex_mono_kernel<<<grid_for(mesh->V * mesh->L), kBlock, 0, s>>>(mesh->V, mesh->L, f->d_zt, f->d_vmono,
+                                                                      f->d_vzero);
     mono_kernel<<<grid_for(mesh->C), kBlock, 0, s>>>(mesh->C, mesh->maxv, mesh->rec_ints, mesh->d_cellrec, f->d_vmono,
-                                                    mesh->L, f->d_mono);
+                                                    f->d_vzero, mesh->L, f->d_mono);
     HIP_TRY(hipGetLastError());
     return MOPS_OK;
 }

@@ -6,6 +6,11 @@ and snapshots are replicated in every GPU's HBM, particles are split into
 contiguous shards, and the only exchange is a gather of the record slabs
 at record instants -- issued on a side stream so it
 overlaps the next segment's kernel.
+
+A rank's ``ParticleSet`` keeps its state and records PHYSICALLY in locality
+(slot) order: slot s holds local particle ``ids[s]``.  Slabs are gathered in
+that order together with each rank's ``ids`` (once per call, after the
+locality sort), and ``unshard_slots`` maps them back to global particle order.
 """
 from __future__ import annotations
 
@@ -52,3 +57,30 @@ def unshard(gathered, n_total: int, world: int):
         import torch
         return torch.cat(parts, dim=-1)
     return np.concatenate(parts, axis=-1)
+
+
+def unshard_slots(gathered, gathered_ids, n_total: int, world: int):
+    """Slot-ordered shards -> [..., n_total] in global particle order.
+
+    ``gathered`` [world, ..., n_pad]: rank r's slab in its slot order;
+    ``gathered_ids`` [world, n_pad]: rank r's ``ParticleSet.ids`` (slot -> local
+    particle index within the rank's shard ``shard_bounds(n_total, r, world)``).
+    """
+    is_torch = hasattr(gathered, "device")
+    if is_torch:
+        import torch
+        out = torch.empty(tuple(gathered.shape[1:-1]) + (int(n_total),), dtype=gathered.dtype, device=gathered.device)
+    else:
+        out = np.empty(tuple(gathered.shape[1:-1]) + (int(n_total),), dtype=gathered.dtype)
+    seen = 0
+    for r in range(world):
+        lo, hi = shard_bounds(n_total, r, world)
+        ids = gathered_ids[r][: hi - lo]
+        ids = ids.long() if is_torch else np.asarray(ids, dtype=np.int64)
+        if hi > lo and (int(ids.min()) < 0 or int(ids.max()) >= hi - lo):
+            raise ValueError(f"rank {r}: slot ids outside its shard")
+        out[..., lo + ids] = gathered[r][..., : hi - lo]
+        seen += hi - lo
+    if seen != n_total:
+        raise ValueError("shards do not cover n_total")
+    return out

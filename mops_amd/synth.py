@@ -253,11 +253,18 @@ class Snapshot:
 
 def make_snapshot(mesh: Mesh, timestep: int = 0, phase: float = 0.0, u0: float = 0.5,
                   u1: float = 0.25, w0: float = 1.0e-5, land_zero: bool = True,
-                  inversions: float = 0.0, inversion_seed: int = 3) -> Snapshot:
+                  inversions: float = 0.0, inversion_seed: int = 3, topography: str = "sigma") -> Snapshot:
     """Solid-body flow + a travelling wave-3 perturbation, decaying with depth.
 
     ``phase`` (radians) shifts the perturbation eastward so consecutive daily
     snapshots form a time-varying (pathline) field.
+
+    ``topography``: "sigma" stretches every layer by (bottom + ssh) / H, so each
+    zTop column strictly decreases to the bottom; "zlevel" is MPAS-O's z-level
+    grid with partial bottom cells: reference thicknesses down to the cell's
+    bottom, the layer holding the bottom cut to it, zero thickness below
+    (inactive levels, maxLevelCell), ssh added to the top layer -- zTop columns
+    then end in flat runs and vertex columns mix cells of different depth.
     """
     C, L = mesh.nCells, mesh.nVertLevels
     lat, lon = mesh.lat_cell, mesh.lon_cell
@@ -267,7 +274,14 @@ def make_snapshot(mesh: Mesh, timestep: int = 0, phase: float = 0.0, u0: float =
     bot = np.clip(bot, 1500.0, H)
     ref_dz = np.diff(np.concatenate([[0.0], mesh.refBottomDepth]))
     ssh = 0.5 * np.cos(lat) * np.sin(2.0 * lon + phase)
-    thick = ref_dz[None, :] * ((bot + ssh) / H)[:, None]
+    if topography == "sigma":
+        thick = ref_dz[None, :] * ((bot + ssh) / H)[:, None]
+    elif topography == "zlevel":
+        top = np.concatenate([[0.0], mesh.refBottomDepth[:-1]])
+        thick = np.clip(bot[:, None] - top[None, :], 0.0, ref_dz[None, :])
+        thick[:, 0] += ssh
+    else:
+        raise ValueError(f"unknown topography {topography!r}")
     if inversions > 0.0:
         # negative / zero layer thicknesses in a fraction of cells: the zTop
         # column is then non-monotone and the reference's fix-up (and the

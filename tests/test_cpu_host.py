@@ -153,7 +153,7 @@ def _gloo_worker(rank, world, port, q):
     try:
         import torch
         from mops_amd import synth
-        from mops_amd.distributed import max_shard, shard_bounds, unshard
+        from mops_amd.distributed import max_shard, shard_bounds, unshard, unshard_slots
         from oracle import oracle as O
         mesh = synth.make_mesh(10, n_levels=8)
         s0 = synth.make_snapshot(mesh)
@@ -170,11 +170,23 @@ def _gloo_worker(rank, world, port, q):
         out = [torch.empty_like(slab) for _ in range(world)]
         dist.all_gather(out, slab)       # gloo has no all_gather_into_tensor on CPU for all versions
         full = unshard(torch.stack(out), len(seeds), world)
+        # the GPU ranks' ParticleSet holds its records in slot (locality) order, slot s = local
+        # particle ids[s]: gather slot-ordered slabs + ids and map them back (unshard_slots)
+        g = torch.Generator().manual_seed(100 + rank)
+        ids = torch.full((npad,), -1, dtype=torch.int32)
+        ids[: hi - lo] = torch.randperm(hi - lo, generator=g).to(torch.int32)
+        slot_slab = slab.clone()
+        slot_slab[..., : hi - lo] = slab[..., ids[: hi - lo].long()]
+        outs = [torch.empty_like(slot_slab) for _ in range(world)]
+        outi = [torch.empty_like(ids) for _ in range(world)]
+        dist.all_gather(outs, slot_slab)
+        dist.all_gather(outi, ids)
+        full_slots = unshard_slots(torch.stack(outs), torch.stack(outi), len(seeds), world)
         if rank == 0:
             ref = O.run(mesh, d0, None, seeds, depth=200.0, delta_t=300, duration=10800, record_t=3600,
                         n_threads=1, finalize=False)
-            ok = (np.array_equal(full[:, :3].numpy().transpose(2, 0, 1), ref["rec_pos"]) and
-                  np.array_equal(full[:, 3:].numpy().transpose(2, 0, 1), ref["rec_vel"]))
+            ok = all(np.array_equal(f[:, :3].numpy().transpose(2, 0, 1), ref["rec_pos"]) and
+                     np.array_equal(f[:, 3:].numpy().transpose(2, 0, 1), ref["rec_vel"]) for f in (full, full_slots))
             q.put(bool(ok))
     finally:
         dist.destroy_process_group()

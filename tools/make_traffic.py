@@ -4,16 +4,25 @@
 gfx950 correction (MI355X_MICROARCH.md §HBM): FETCH_SIZE (KiB) counts half the
 bytes of 16-B-per-lane reads, so bytes = 2 x FETCH_SIZE (the raw value is kept
 beside it); WRITE_SIZE (KiB) is taken as is.  Both are L2 memory-side counters
-(Infinity-Cache hits included)."""
+(Infinity-Cache hits included).  Each record carries the engine build id
+(bench.engine_build_id: source + flags hash) it was measured on; bench.py uses
+a record only for that build.
+
+Usage: python tools/make_traffic.py PROFILE_DIR WORKLOAD_KEY profiles/pmc_traffic.json [LABEL]
+"""
 import csv, glob, json, os, statistics, sys
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+import bench  # noqa: E402
 out = sys.argv[1]; workload = sys.argv[2]; dst = sys.argv[3]
+label = sys.argv[4] if len(sys.argv) > 4 else out
 def mean(counter, d):
     v = [float(r["Counter_Value"]) for f in glob.glob(f"{out}/{d}/**/*counter_collection.csv", recursive=True)
          for r in csv.DictReader(open(f)) if "traj_kernel" in r["Kernel_Name"] and r["Counter_Name"] == counter]
     return statistics.mean(v), len(v)
 fetch, nf = mean("FETCH_SIZE", "fetch")
 write, nw = mean("WRITE_SIZE", "write")
-rec = dict(workload=workload, fetch_size_kib=fetch, write_size_kib=write, dispatches=[nf, nw],
+rec = dict(workload=workload, engine_build=bench.engine_build_id(), profile=label,
+           fetch_size_kib=fetch, write_size_kib=write, dispatches=[nf, nw],
            bytes_per_launch=(2.0 * fetch + write) * 1024.0,
            note="bytes_per_launch = (2*FETCH_SIZE + WRITE_SIZE)*1024 per traj_kernel dispatch (gfx950 FETCH_SIZE correction)")
 recs = []
