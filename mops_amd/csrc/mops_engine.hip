@@ -148,8 +148,91 @@ __device__ __forceinline__ unsigned long long* stamp_slot() {
 #if defined(MOPS_ABL_SQRT)
 __device__ __forceinline__ double xsqrt(double x) { return x * __builtin_amdgcn_rsq(x); }
 #else
-__device__ __forceinline__ double xsqrt(double x) { return sqrt(x); }
+// Correctly rounded sqrt, bit-identical to the compiler's sqrt(): for x in
+// [2^-767, inf) its gfx950 expansion is exactly this rsq + Newton/Markstein
+// sequence -- the input/output ldexp scaling (for x < 2^-767) and the +-0/+inf
+// select around it are then identities, so they are skipped here.  Other x
+// (0, tiny, inf, NaN, negative) take sqrt() itself.  Checked bitwise against
+// sqrt() on the device and the host (mops_selftest_math, tests/test_gpu_parity.py).
+__device__ __forceinline__ double sqrt_core(double x) {
+    const double y = __builtin_amdgcn_rsq(x);
+    double g = x * y;
+    double h = y * 0.5;
+    double r = __builtin_fma(-h, g, 0.5);
+    g = __builtin_fma(g, r, g);
+    h = __builtin_fma(h, r, h);
+    double d = __builtin_fma(-g, g, x);
+    g = __builtin_fma(d, h, g);
+    d = __builtin_fma(-g, g, x);
+    return __builtin_fma(d, h, g);
+}
+#ifndef MOPS_FAST_SQRT
+#define MOPS_FAST_SQRT 1
 #endif
+__device__ __forceinline__ double xsqrt(double x) {
+#if MOPS_FAST_SQRT
+    if (__builtin_expect(x >= 0x1p-767 && x < __builtin_huge_val(), 1)) return sqrt_core(x);
+#endif
+    return sqrt(x);
+}
+#endif
+
+// An FP64 constant materialised in an SGPR pair at its point of use.  Plain
+// literals are loop-invariant, so the compiler hoists them out of the step
+// loop into VGPR pairs -- which at this kernel's register pressure are
+// spilled to scratch and re-loaded from memory every step.  The s_mov_b32
+// pair takes a loop-variant uniform input (`salt`, the step index) that it
+// ignores, so it cannot be hoisted, yet (not volatile) it schedules freely.
+__device__ __forceinline__ double kconst(unsigned hi, unsigned lo, unsigned salt) {
+    unsigned h, l;
+    asm("s_mov_b32 %0, %1" : "=s"(l) : "i"(lo), "s"(salt));
+    asm("s_mov_b32 %0, %1" : "=s"(h) : "i"(hi), "s"(salt));
+    return __hiloint2double((int)h, (int)l);
+}
+#define MOPS_K(bits) dev::kconst((unsigned)((bits) >> 32), (unsigned)((bits) & 0xffffffffULL), salt)
+
+// sin and cos of |x| < 0.78, bit-identical to the device library's sin(x) / cos(x):
+// their gfx950 expansion reduces x by k = rint(|x| * 2/pi) with a Cody-Waite
+// chain that, for k = 0, returns r = |x| and rr = +0 exactly, evaluates both
+// kernel polynomials and selects by quadrant; sin takes the sign of x.  This is
+// that k = 0 path with the same operations in the same order (the rr terms kept
+// as literal +-0), skipping the reduction and the second polynomial of each
+// call.  Checked bitwise against sin()/cos() (mops_selftest_math).
+__device__ __forceinline__ void sincos_small(double x, double& s, double& c, unsigned salt) {
+    const double r = fabs(x), rr = 0.0;
+    const double x2 = r * r;
+    const double h = x2 * 0.5;
+    double t16 = __builtin_fma(MOPS_K(0xbda907db46cc5e42ULL), x2, MOPS_K(0x3e21eeb69037ab78ULL));
+    const double t12 = 1.0 - h;
+    double t18 = __builtin_fma(x2, t16, MOPS_K(0xbe927e4fa17f65f6ULL));
+    const double t14 = 1.0 - t12;
+    t16 = __builtin_fma(x2, t18, MOPS_K(0x3efa01a019f4ec90ULL));
+    double t10 = t14 - h;
+    t18 = __builtin_fma(x2, t16, MOPS_K(0xbf56c16c16c16967ULL));
+    const double x4 = x2 * x2;
+    t16 = __builtin_fma(x2, t18, MOPS_K(0x3fa5555555555555ULL));
+    t10 = __builtin_fma(r, -rr, t10);
+    t10 = __builtin_fma(x4, t16, t10);
+    c = t12 + t10;
+    double u12 = __builtin_fma(MOPS_K(0x3de5e0b2f9a43bb8ULL), x2, MOPS_K(0xbe5ae600b42fdfa7ULL));
+    double u14 = __builtin_fma(x2, u12, MOPS_K(0x3ec71de3796cde01ULL));
+    u12 = __builtin_fma(x2, u14, MOPS_K(0xbf2a01a019e83e5cULL));
+    u14 = __builtin_fma(x2, u12, MOPS_K(0x3f81111111110bb3ULL));
+    u12 = r * -x2;
+    double u16 = rr * 0.5;
+    u16 = __builtin_fma(u12, u14, u16);
+    double u4 = __builtin_fma(x2, u16, -rr);
+    u4 = __builtin_fma(MOPS_K(0xbfc5555555555555ULL), u12, u4);
+    const double sv = r - u4;
+    s = __longlong_as_double(__double_as_longlong(sv) ^ (__double_as_longlong(x) & (long long)0x8000000000000000ULL));
+}
+
+// The library sin/cos for the rare |x| >= 0.78, out of line so that its
+// constants are not hoisted into the step loop.
+__device__ __attribute__((noinline)) void sincos_lib(double x, double* s, double* c) {
+    *c = cos(x);
+    *s = sin(x);
+}
 #if defined(MOPS_ABL_DIV)
 __device__ __forceinline__ double xdiv(double a, double b) { return a * __builtin_amdgcn_rcp(b); }
 #else
@@ -178,12 +261,20 @@ __device__ __forceinline__ double tri_area(double ax, double ay, double az, doub
 }
 
 // TBBKernel::CalcPositionAfterRotation (TBBKernel.h:177-206)
-__device__ __forceinline__ void rotate(double px, double py, double pz, double ax, double ay, double az, double th,
+__device__ __forceinline__ void rotate(unsigned salt, double px, double py, double pz, double ax, double ay, double az, double th,
                                        double& rx, double& ry, double& rz) {
 #if defined(MOPS_ABL_TRIG)
     const double c = 1.0 - 0.5 * th * th, s = th;
 #else
-    const double c = cos(th), s = sin(th);
+    double c, s;
+#ifndef MOPS_FAST_TRIG
+#define MOPS_FAST_TRIG 1
+#endif
+    if (MOPS_FAST_TRIG && __builtin_expect(fabs(th) < 0.78, 1)) {
+        sincos_small(th, s, c, salt);
+    } else {
+        sincos_lib(th, &s, &c);
+    }
 #endif
     const double al = len3(ax, ay, az);
     if (al <= 1e-12) { rx = px; ry = py; rz = pz; return; }
@@ -194,13 +285,13 @@ __device__ __forceinline__ void rotate(double px, double py, double pz, double a
 }
 
 // advect_on_sphere lambda (MPASOVisualizerKernels.cpp:729-738)
-__device__ __forceinline__ void advect(double px, double py, double pz, double vx, double vy, double vz, double dt,
+__device__ __forceinline__ void advect(unsigned salt, double px, double py, double pz, double vx, double vy, double vz, double dt,
                                        double& ox, double& oy, double& oz) {
     const double rr = len3(px, py, pz), sp = len3(vx, vy, vz);
     if (rr < 1e-12 || sp < 1e-12) { ox = px; oy = py; oz = pz; return; }
     const double ax = py * vz - pz * vy, ay = pz * vx - px * vz, az = px * vy - py * vx;
     const double th = (sp * dt) / rr;
-    rotate(px, py, pz, ax, ay, az, th, ox, oy, oz);
+    rotate(salt, px, py, pz, ax, ay, az, th, ox, oy, oz);
 }
 
 __device__ __forceinline__ double dmax(double a, double b) { return (a < b) ? b : a; }  // std::max
@@ -770,7 +861,9 @@ __device__ __forceinline__ void pair_sums(const Cell<MAXV>& c, const double* w, 
 // the surface" test d > z_0 + eps first.  That test needs no z_0 in the
 // record: for h == 1, z_0 = z_{h-1}; for h >= 2 the accepted case has d <
 // z_{h-1} - eps < z_0 - eps (strictly decreasing prefix), so d > z_0 + eps is
-// false there.  Otherwise bracket_mono walks from the hint inside the prefix,
+// false there.  A particle below the bottom of a fully decreasing column
+// (km = L-1) is accepted at h = L-1 the same way (the reference's "below the
+// bottom" branch).  Otherwise bracket_mono walks from the hint inside the prefix,
 // and bracket_scan (the whole fixed-up column) runs when the walk would leave
 // it; the record of the final layer is then read.
 template <int MAXV, bool PATH, int GR>
@@ -782,6 +875,11 @@ __device__ __forceinline__ int layer_eval(const Cell<MAXV>& c, const double* w, 
         pair_sums<MAXV, GR>(c, w, f.pr, L, h, S);
         bool ok;
         if (h == 1 && d > S.zm + eps) {  // above the surface (z_0 = z_{h-1} here)
+            ok = true;
+        } else if (h == L - 1 && km == L - 1 && d < S.zk - eps) {
+            // below the bottom: !Q(L-1) with the whole column decreasing -- the
+            // reference's "below the bottom" branch, layer L-1 with z'_{L-1} = z_{L-1}
+            // and z'_{L-2} = z_{L-2} (bracket_mono's not-found case)
             ok = true;
         } else {
             const bool Qh = d >= S.zk - eps;
@@ -1025,7 +1123,7 @@ __global__ void __launch_bounds__(kTrajBlock, (TrajWaves<MAXV, PATH, EULER>::val
             const double ax = y * hz - z * hy, ay = z * hx - x * hz, az = x * hy - y * hx;
             const double speed = dev::len3(hx, hy, hz);
             const double th = (speed * a.delta_t) / dev::dmax(1e-12, r);
-            dev::rotate(x, y, z, ax, ay, az, th, nx, ny, nz);
+            dev::rotate((unsigned)step, x, y, z, ax, ay, az, th, nx, ny, nz);
         } else {
             const double dt = (double)a.delta_t;
             double s1x, s1y, s1z, s1w, s2x, s2y, s2z, s2w, s3x, s3y, s3z, s3w, s4x, s4y, s4z, s4w;
@@ -1034,16 +1132,16 @@ __global__ void __launch_bounds__(kTrajBlock, (TrajWaves<MAXV, PATH, EULER>::val
             bool ok = PATH ? dev::eval_path<MAXV, PairGroup<PATH, EULER>::value>(c, a.L, a.V, a.f0, a.f1, x, y, z, d, a1, hint0, hint1, s1x, s1y, s1z, s1w)
                            : dev::eval_stream<MAXV, PairGroup<PATH, EULER>::value>(c, a.L, a.V, a.f0, x, y, z, d, hint0, s1x, s1y, s1z, s1w);
             if (!ok) { died = (int)step; break; }
-            dev::advect(x, y, z, s1x, s1y, s1z, dt * 0.5, qx, qy, qz);
+            dev::advect((unsigned)step, x, y, z, s1x, s1y, s1z, dt * 0.5, qx, qy, qz);
             const double a2 = PATH ? dev::dclamp(a1 + 0.5 * a.dalpha, 0.0, 1.0) : 0.0;
             ok = PATH ? dev::eval_path<MAXV, PairGroup<PATH, EULER>::value>(c, a.L, a.V, a.f0, a.f1, qx, qy, qz, d, a2, hint0, hint1, s2x, s2y, s2z, s2w)
                       : dev::eval_stream<MAXV, PairGroup<PATH, EULER>::value>(c, a.L, a.V, a.f0, qx, qy, qz, d, hint0, s2x, s2y, s2z, s2w);
             if (!ok) { died = (int)step; break; }
-            dev::advect(x, y, z, s2x, s2y, s2z, dt * 0.5, qx, qy, qz);
+            dev::advect((unsigned)step, x, y, z, s2x, s2y, s2z, dt * 0.5, qx, qy, qz);
             ok = PATH ? dev::eval_path<MAXV, PairGroup<PATH, EULER>::value>(c, a.L, a.V, a.f0, a.f1, qx, qy, qz, d, a2, hint0, hint1, s3x, s3y, s3z, s3w)
                       : dev::eval_stream<MAXV, PairGroup<PATH, EULER>::value>(c, a.L, a.V, a.f0, qx, qy, qz, d, hint0, s3x, s3y, s3z, s3w);
             if (!ok) { died = (int)step; break; }
-            dev::advect(x, y, z, s3x, s3y, s3z, dt, qx, qy, qz);
+            dev::advect((unsigned)step, x, y, z, s3x, s3y, s3z, dt, qx, qy, qz);
             const double a4 = PATH ? dev::dclamp(a1 + a.dalpha, 0.0, 1.0) : 0.0;
             ok = PATH ? dev::eval_path<MAXV, PairGroup<PATH, EULER>::value>(c, a.L, a.V, a.f0, a.f1, qx, qy, qz, d, a4, hint0, hint1, s4x, s4y, s4z, s4w)
                       : dev::eval_stream<MAXV, PairGroup<PATH, EULER>::value>(c, a.L, a.V, a.f0, qx, qy, qz, d, hint0, s4x, s4y, s4z, s4w);
@@ -1089,6 +1187,22 @@ __global__ void __launch_bounds__(kTrajBlock, (TrajWaves<MAXV, PATH, EULER>::val
     a.depth[pid] = dep;
     a.cell[pid] = cell;
     if (died >= 0) a.death[pid] = died;
+}
+
+// exact math helpers against the library (mops_selftest_math)
+__global__ void selftest_math_kernel(int64_t n, const double* __restrict__ x, double* __restrict__ out, int op) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const double v = x[i];
+    if (op == 0) {
+        out[2 * i] = dev::xsqrt(v);
+        out[2 * i + 1] = sqrt(v);
+    } else {
+        const double ls = sin(v), lc = cos(v);
+        double s = ls, c = lc;
+        if (fabs(v) < 0.78) dev::sincos_small(v, s, c, (unsigned)i);
+        out[4 * i] = s; out[4 * i + 1] = ls; out[4 * i + 2] = c; out[4 * i + 3] = lc;
+    }
 }
 
 // ===========================================================================
@@ -1703,6 +1817,15 @@ int mops_debug_stamps(unsigned long long* d_buf, long long cap, int* occ) {
 }
 #endif
 int32_t mops_abi_version(void) { return MOPS_ABI_VERSION; }
+
+mops_status mops_selftest_math(int64_t n, const double* d_x, double* d_out, int32_t op, void* stream) {
+    if (n < 0 || (n > 0 && (!d_x || !d_out)) || (op != 0 && op != 1))
+        return fail(MOPS_ERR_INVALID, "mops_selftest_math: bad arguments");
+    if (n == 0) return MOPS_OK;
+    selftest_math_kernel<<<grid_for(n), kBlock, 0, (hipStream_t)stream>>>(n, d_x, d_out, op);
+    HIP_TRY(hipGetLastError());
+    return MOPS_OK;
+}
 
 mops_status mops_mesh_create(const mops_mesh_desc* desc, void* stream, mops_mesh** out) {
     if (!desc || !out) return fail(MOPS_ERR_INVALID, "mops_mesh_create: null argument");

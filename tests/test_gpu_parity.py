@@ -68,6 +68,37 @@ def test_device_math_matches_host(gpu):
     assert np.array_equal((torch.as_tensor(y, device=gpu) / t).cpu().numpy(), y / x)
 
 
+def test_fast_math_helpers_match_library(gpu, engine_lib):
+    """The kernel's exact sqrt and small-angle sincos (dev::xsqrt, dev::sincos_small) must
+    give the device library's sqrt/sin/cos bit for bit; the library's correctly rounded
+    sqrt must also equal the host's."""
+    import ctypes
+    import torch
+    rng = np.random.default_rng(10)
+    x = np.concatenate([10.0 ** rng.uniform(-320, 308, 400000), rng.uniform(0, 1e14, 200000),
+                        np.array([0.0, -0.0, 5e-324, 2.0 ** -767, np.nextafter(2.0 ** -767, 0), np.inf, -1.0,
+                                  np.nan, 1e-24, 4.0e13])])
+    d = torch.as_tensor(x, device=gpu)
+    out = torch.empty((len(x), 2), dtype=torch.float64, device=gpu)
+    assert engine_lib.mops_selftest_math(len(x), ctypes.c_void_p(d.data_ptr()), ctypes.c_void_p(out.data_ptr()), 0,
+                                         None) == 0
+    o = out.cpu().numpy()
+    assert np.array_equal(o[:, 0].view(np.int64), o[:, 1].view(np.int64)), "fast sqrt != sqrt()"
+    fin = np.isfinite(x) & (x >= 0)
+    assert np.array_equal(o[fin, 1], np.sqrt(x[fin]))
+    th = np.concatenate([rng.uniform(-0.78, 0.78, 400000),
+                         np.sign(rng.uniform(-1, 1, 400000)) * 10.0 ** rng.uniform(-14, np.log10(0.78), 400000),
+                         rng.uniform(-1e-4, 1e-4, 1000000), np.array([0.0, -0.0, 0.7799999, -0.7799999, 1e-300])])
+    d = torch.as_tensor(th, device=gpu)
+    out = torch.empty((len(th), 4), dtype=torch.float64, device=gpu)
+    assert engine_lib.mops_selftest_math(len(th), ctypes.c_void_p(d.data_ptr()), ctypes.c_void_p(out.data_ptr()), 1,
+                                         None) == 0
+    o = out.cpu().numpy()
+    assert np.array_equal(o[:, 0].view(np.int64), o[:, 1].view(np.int64)), "fast sin != sin()"
+    assert np.array_equal(o[:, 2].view(np.int64), o[:, 3].view(np.int64)), "fast cos != cos()"
+    print(f"device sin == host sin: {np.mean(o[:, 1] == np.sin(th)):.6f}, cos: {np.mean(o[:, 3] == np.cos(th)):.6f}")
+
+
 def test_preprocessing_bitwise(dev_small, ref_small, small_case):
     mesh, s0, s1 = small_case
     _, f0, _ = dev_small
