@@ -72,6 +72,10 @@ def parse():
                    help="integration steps per kernel launch (config 2: whole record periods; 0 = the whole "
                         "run at N=1, a quarter of it at N>1 so record all-gathers overlap the next launch; "
                         "chains: 0 = launches of 3 simulated days with a locality re-sort between them)")
+    p.add_argument("--parts", type=int, default=2,
+                   help="config 2: particle parts on their own streams (ParticleSet.advance_pipelined)")
+    p.add_argument("--chunks", type=int, default=6,
+                   help="config 2: step chunks per part and segment (shorter launches whose tails overlap)")
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--cpu-seconds", type=float, default=12.0, help="target CPU-baseline sample length")
     return p.parse_args()
@@ -139,17 +143,18 @@ def measured_traffic(key: str):
             continue
         if e.get("engine_build") != bid:
             return None, f"stale: the PMC entry for {key} was measured on engine build {e.get('engine_build')}, not {bid}"
-        return float(e["bytes_per_launch"]), (f"profiles/pmc_traffic.json[{key}] (rocprofv3 2*FETCH_SIZE + WRITE_SIZE "
-                                               f"per launch, engine build {bid}, {e.get('profile', '?')})")
+        return float(e["bytes_per_unit"]), (f"profiles/pmc_traffic.json[{key}] (rocprofv3 2*FETCH_SIZE + WRITE_SIZE "
+                                             f"per timed unit, engine build {bid}, {e.get('profile', '?')})")
     return None, f"no PMC entry for {key}"
 
 
-def roofline_block(kernel: str, avg_kernel_s: float, psteps_per_launch: float, B: float, traffic_key: str) -> dict:
+def roofline_block(kernel: str, avg_kernel_s: float, psteps_per_launch: float, B: float, traffic_key: str,
+                   per: str = "launch") -> dict:
     """The bench line's roofline: HBM GB/s MEASURED by rocprofv3 PMC counters (per launch) over the
     kernel's HIP-event launch time, against the 8 TB/s peak.  The SURVEY 8(d) bytes model is reported
     beside it, not as the roofline: it charges a full zTop column and no cross-particle reuse, so its
     rate exceeds the HBM peak -- the kernel is bound by gather latency and FP64 issue, not by DRAM."""
-    traffic, src = measured_traffic(traffic_key)
+    traffic, src = measured_traffic(traffic_key)  # bytes per `per` unit
     achieved = traffic / avg_kernel_s / 1e9 if traffic is not None else None
     alg = B * psteps_per_launch / avg_kernel_s / 1e9
     return {
@@ -163,6 +168,7 @@ def roofline_block(kernel: str, avg_kernel_s: float, psteps_per_launch: float, B
         "limiter": ("not DRAM: dependent per-lane gathers (L1/TA-served) and FP64 VALU issue at 3 waves/SIMD "
                     "(DESIGN.md section 3)"),
         "kernel": kernel,
+        "timed_unit": per,
         "particle_steps_per_launch": psteps_per_launch,
         "avg_launch_ms": avg_kernel_s * 1e3,
         "algorithmic_model": {
@@ -254,6 +260,7 @@ def main():
     segments = [(bounds[i], bounds[i + 1]) for i in range(len(bounds) - 1)]
     compute = torch.cuda.Stream(dev)
     comm = torch.cuda.Stream(dev)
+    part_streams = [torch.cuda.Stream(dev) for _ in range(max(1, args.parts))]
     gathered = gathered_ids = None
     if world > 1:
         # records are gathered in each rank's slot (locality) order, with the rank's slot -> particle
@@ -277,12 +284,17 @@ def main():
                 with torch.cuda.stream(comm):
                     all_gather_flat(dist, gathered_ids.view(-1), ps.ids, args.backend)
             for (s0, s1) in segments:
+                # the segment's trajectory launches: particle parts on their own streams, each in
+                # step chunks, so one part's final partial round of waves overlaps the others' work
+                e0 = torch.cuda.Event(enable_timing=True); e1 = torch.cuda.Event(enable_timing=True)
+                e0.record(compute)
+                for st in part_streams:
+                    st.wait_event(e0)
+                ps.advance_pipelined(dfield, dback, s0, s1, part_streams, args.chunks)
+                for st in part_streams:
+                    j = torch.cuda.Event(); j.record(st); compute.wait_event(j)
+                e1.record(compute)
                 if timed:
-                    e0 = torch.cuda.Event(enable_timing=True); e1 = torch.cuda.Event(enable_timing=True)
-                    e0.record(compute)
-                ps.advance(dfield, dback, s0, s1, stream=compute)
-                if timed:
-                    e1.record(compute)
                     kernel_ms.append((e0, e1))
                 if world > 1:  # the records this segment completed, gathered while the next one computes
                     k0, k1 = s0 // period, min(s1 // period, ps.K)
@@ -332,7 +344,9 @@ def main():
     psteps_per_launch = attempted / len(segments)
     roof = roofline_block(f"traj_kernel<7,{str(pathline).lower()},{str(args.method == 'euler').lower()}> "
                           f"({args.mode} {args.method})", avg_kernel_s, psteps_per_launch, B,
-                          f"ec30to60_{args.mode}_{args.method}_{args.particles}_seg{seg}")
+                          f"ec30to60_{args.mode}_{args.method}_{args.particles}_seg{seg}_p{args.parts}c{args.chunks}",
+                          per=f"segment ({args.parts} particle parts x {args.chunks} step chunks = "
+                              f"{args.parts * args.chunks} overlapping traj_kernel launches)")
 
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:

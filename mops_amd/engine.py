@@ -349,6 +349,52 @@ class ParticleSet:
         L.check(st, "mops_traj_advance")
         self._written = True
 
+    def _sub_particles(self, lo: int, hi: int) -> L.Particles:
+        e4, e8 = 4, 8
+        return L.Particles(hi - lo, self.x.data_ptr() + e8 * lo, self.y.data_ptr() + e8 * lo,
+                           self.z.data_ptr() + e8 * lo, self.depth.data_ptr() + e4 * lo,
+                           self.cell.data_ptr() + e4 * lo, self.death.data_ptr() + e4 * lo, None)
+
+    def advance_pipelined(self, front: DeviceField, back: DeviceField | None, step_begin: int, step_end: int,
+                          streams, chunks: int, timing=None):
+        """``advance`` split into len(streams) contiguous particle parts (whole waves), each on its own
+        stream, and ``chunks`` step ranges per part, enqueued chunk-major.
+
+        One launch over all particles ends in a partial round of waves: 1e6 particles are 15625
+        waves over 3072 resident slots (5.09 rounds), so the last 9% of a round runs alone for a
+        whole wave lifetime.  Shorter launches on several streams let one part's tail overlap the
+        other parts' next chunk (kernel boundaries order each part's chunks; results are
+        identical for any split: every particle is independent and records are indexed by
+        absolute step).  The streams must already be ordered after the state's producers; the
+        caller joins them afterwards.  ``timing`` receives (start, end) events per launch."""
+        torch = self.torch
+        nparts = max(1, len(streams))
+        waves = -(-self.n // 64)
+        pb = [min(self.n, 64 * (waves * k // nparts)) for k in range(nparts + 1)]
+        span = int(step_end) - int(step_begin)
+        chunks = max(1, min(int(chunks), span))
+        tb = [int(step_begin) + span * k // chunks for k in range(chunks + 1)]
+        lib = L.load()
+        for t in range(chunks):
+            for k in range(nparts):
+                lo, hi = pb[k], pb[k + 1]
+                if hi <= lo or tb[t + 1] <= tb[t]:
+                    continue
+                st = streams[k]
+                if timing is not None:
+                    e0 = torch.cuda.Event(enable_timing=True); e1 = torch.cuda.Event(enable_timing=True)
+                    e0.record(st)
+                p = self._sub_particles(lo, hi)
+                rc = lib.mops_traj_advance(self.mesh.handle, front.handle, None if back is None else back.handle,
+                                           C.byref(self._c), C.byref(p), tb[t], tb[t + 1],
+                                           C.c_void_p(self.records.data_ptr() + 8 * lo), self.n,
+                                           _stream_handle(st))
+                L.check(rc, "mops_traj_advance")
+                if timing is not None:
+                    e1.record(st)
+                    timing.append((e0, e1))
+        self._written = True
+
     def record_period(self, pathline: bool) -> int:
         import math
         if pathline:

@@ -229,6 +229,31 @@ def test_segmented_advance_equals_single(gpu, dev_small, small_case):
     assert torch.equal(a.x, b.x) and torch.equal(a.death, b.death) and torch.equal(a.depth, b.depth)
 
 
+def test_pipelined_advance_equals_single(gpu, dev_small, small_case):
+    """ParticleSet.advance_pipelined (particle parts on 3 streams x 5 step chunks, the bench's
+    config-2 schedule) gives the single launch's records and state bit for bit."""
+    import torch
+    from mops_amd import synth
+    from mops_amd.engine import ParticleSet, TrajectoryConfig
+    dm, f0, f1 = dev_small
+    seeds = synth.uniform_band_seeds(3001, seed=18)
+    for back, method in ((None, 1), (f1, 0)):
+        cfg = TrajectoryConfig(deltaT=120, simulationDuration=43200, recordT=3600, depth=350.0, method=method)
+        a = ParticleSet(dm, seeds, 350.0, cfg)
+        a.advance(f0, back, 0, cfg.n_steps)
+        b = ParticleSet(dm, seeds, 350.0, cfg)
+        streams = [torch.cuda.Stream() for _ in range(3)]
+        for st in streams:
+            st.wait_stream(torch.cuda.current_stream())
+        b.advance_pipelined(f0, back, 0, cfg.n_steps, streams, 5)
+        for st in streams:
+            torch.cuda.current_stream().wait_stream(st)
+        torch.cuda.synchronize()
+        assert torch.equal(a.records, b.records)
+        for k in ("x", "y", "z", "depth", "cell", "death"):
+            assert torch.equal(getattr(a, k), getattr(b, k)), k
+
+
 def test_medium_mesh_l60_parity(gpu, engine_lib, medium_case, oracle_lib):
     """EC30to60-like vertical grid (60 levels): exercises the streaming bracket."""
     from mops_amd import synth

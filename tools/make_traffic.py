@@ -8,23 +8,28 @@ beside it); WRITE_SIZE (KiB) is taken as is.  Both are L2 memory-side counters
 (bench.engine_build_id: source + flags hash) it was measured on; bench.py uses
 a record only for that build.
 
-Usage: python tools/make_traffic.py PROFILE_DIR WORKLOAD_KEY profiles/pmc_traffic.json [LABEL]
+Usage: python tools/make_traffic.py PROFILE_DIR WORKLOAD_KEY profiles/pmc_traffic.json UNITS [LABEL]
+UNITS = how many of bench.py's timed units (roofline.timed_unit: a launch, or a config-2
+segment of overlapping part x chunk launches) the profiled run executed; the record's
+bytes_per_unit = all traj_kernel bytes of the run / UNITS.
 """
 import csv, glob, json, os, statistics, sys
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 import bench  # noqa: E402
 out = sys.argv[1]; workload = sys.argv[2]; dst = sys.argv[3]
-label = sys.argv[4] if len(sys.argv) > 4 else out
-def mean(counter, d):
+units = float(sys.argv[4])
+label = sys.argv[5] if len(sys.argv) > 5 else out
+def total(counter, d):
     v = [float(r["Counter_Value"]) for f in glob.glob(f"{out}/{d}/**/*counter_collection.csv", recursive=True)
          for r in csv.DictReader(open(f)) if "traj_kernel" in r["Kernel_Name"] and r["Counter_Name"] == counter]
-    return statistics.mean(v), len(v)
-fetch, nf = mean("FETCH_SIZE", "fetch")
-write, nw = mean("WRITE_SIZE", "write")
+    return sum(v), len(v)
+fetch, nf = total("FETCH_SIZE", "fetch")
+write, nw = total("WRITE_SIZE", "write")
 rec = dict(workload=workload, engine_build=bench.engine_build_id(), profile=label,
-           fetch_size_kib=fetch, write_size_kib=write, dispatches=[nf, nw],
-           bytes_per_launch=(2.0 * fetch + write) * 1024.0,
-           note="bytes_per_launch = (2*FETCH_SIZE + WRITE_SIZE)*1024 per traj_kernel dispatch (gfx950 FETCH_SIZE correction)")
+           fetch_size_kib_total=fetch, write_size_kib_total=write, dispatches=[nf, nw], units=units,
+           bytes_per_unit=(2.0 * fetch + write) * 1024.0 / units,
+           note="bytes_per_unit = (2*FETCH_SIZE + WRITE_SIZE)*1024 summed over the run's traj_kernel dispatches / units "
+                "(gfx950 FETCH_SIZE correction)")
 recs = []
 if os.path.exists(dst):
     old = json.load(open(dst))
