@@ -1004,7 +1004,7 @@ struct TrajArgs {
 #define MOPS_W_SR 1  // streamline RK4
 #endif
 #ifndef MOPS_W_PE
-#define MOPS_W_PE 1  // pathline Euler
+#define MOPS_W_PE 3  // pathline Euler (at 1 the compiler takes 172 VGPRs = 2 waves: -9.5% at config 2's mesh)
 #endif
 #ifndef MOPS_W_PR
 #define MOPS_W_PR 2  // pathline RK4
