@@ -229,9 +229,10 @@ __device__ __forceinline__ void sincos_small(double x, double& s, double& c, uns
 
 // The library sin/cos for the rare |x| >= 0.78, out of line so that its
 // constants are not hoisted into the step loop.
-__device__ __attribute__((noinline)) void sincos_lib(double x, double* s, double* c) {
-    *c = cos(x);
-    *s = sin(x);
+// (Returned by value: out-pointers to the caller's locals would pin them in
+// scratch memory on every step, fast path included.)
+__device__ __attribute__((noinline)) double2 sincos_lib(double x) {
+    return make_double2(sin(x), cos(x));
 }
 #if defined(MOPS_ABL_DIV)
 __device__ __forceinline__ double xdiv(double a, double b) { return a * __builtin_amdgcn_rcp(b); }
@@ -273,7 +274,9 @@ __device__ __forceinline__ void rotate(unsigned salt, double px, double py, doub
     if (MOPS_FAST_TRIG && __builtin_expect(fabs(th) < 0.78, 1)) {
         sincos_small(th, s, c, salt);
     } else {
-        sincos_lib(th, &s, &c);
+        const double2 sc = sincos_lib(th);
+        s = sc.x;
+        c = sc.y;
     }
 #endif
     const double al = len3(ax, ay, az);

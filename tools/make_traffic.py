@@ -17,7 +17,7 @@ import csv, glob, json, os, statistics, sys
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 import bench  # noqa: E402
 out = sys.argv[1]; workload = sys.argv[2]; dst = sys.argv[3]
-units = float(sys.argv[4])
+units_arg = sys.argv[4]  # a number, or "dispatches" (the bench's timed unit is one launch)
 label = sys.argv[5] if len(sys.argv) > 5 else out
 def total(counter, d):
     v = [float(r["Counter_Value"]) for f in glob.glob(f"{out}/{d}/**/*counter_collection.csv", recursive=True)
@@ -25,6 +25,7 @@ def total(counter, d):
     return sum(v), len(v)
 fetch, nf = total("FETCH_SIZE", "fetch")
 write, nw = total("WRITE_SIZE", "write")
+units = float(nf) if units_arg == "dispatches" else float(units_arg)
 rec = dict(workload=workload, engine_build=bench.engine_build_id(), profile=label,
            fetch_size_kib_total=fetch, write_size_kib_total=write, dispatches=[nf, nw], units=units,
            bytes_per_unit=(2.0 * fetch + write) * 1024.0 / units,
