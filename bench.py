@@ -270,6 +270,7 @@ def main():
     seeds_dev = ps.seeds
 
     kernel_ms = []
+    dispatch_ms = []  # per traj_kernel launch (HIP events on its part stream): what rocprofv3 averages
 
     def one_call(timed: bool):
         """One StreamLine call on this rank's shard (device resident)."""
@@ -290,7 +291,8 @@ def main():
                 e0.record(compute)
                 for st in part_streams:
                     st.wait_event(e0)
-                ps.advance_pipelined(dfield, dback, s0, s1, part_streams, args.chunks)
+                ps.advance_pipelined(dfield, dback, s0, s1, part_streams, args.chunks,
+                                     timing=dispatch_ms if timed else None)
                 for st in part_streams:
                     j = torch.cuda.Event(); j.record(st); compute.wait_event(j)
                 e1.record(compute)
@@ -328,6 +330,7 @@ def main():
     dead = int((death >= 0).sum().item())
     kms = [a.elapsed_time(b) for (a, b) in kernel_ms]
     avg_kernel_s = (sum(kms) / len(kms)) / 1e3 if kms else float("nan")
+    dms = [a.elapsed_time(b) for (a, b) in dispatch_ms]
     stats = torch.tensor([elapsed, float(attempted), float(n), float(dead)], dtype=torch.float64,
                          device=dev if args.backend == "nccl" else "cpu")
     if world > 1:
@@ -347,6 +350,8 @@ def main():
                           f"ec30to60_{args.mode}_{args.method}_{args.particles}_seg{seg}_p{args.parts}c{args.chunks}",
                           per=f"segment ({args.parts} particle parts x {args.chunks} step chunks = "
                               f"{args.parts * args.chunks} overlapping traj_kernel launches)")
+    roof["dispatches_per_unit"] = len(dms) // max(1, args.steps * len(segments))
+    roof["avg_dispatch_ms"] = (sum(dms) / len(dms)) if dms else None  # = rocprofv3's traj_kernel average
 
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
