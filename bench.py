@@ -76,6 +76,11 @@ def parse():
                    help="config 2: particle parts on their own streams (ParticleSet.advance_pipelined)")
     p.add_argument("--chunks", type=int, default=6,
                    help="config 2: step chunks per part and segment (shorter launches whose tails overlap)")
+    p.add_argument("--gather", choices=["checkpoint", "records"], default="checkpoint",
+                   help="config 2, N > 1: 'checkpoint' = one all-gather per call of every particle's final state "
+                        "(position, depth, death) + slot ids -- particles are independent, so the path itself "
+                        "needs no exchange and each rank keeps its shard's records; 'records' = all-gather every "
+                        "record slab as well (1.15 GB per rank per call), overlapped with the next quarter run")
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--cpu-seconds", type=float, default=12.0, help="target CPU-baseline sample length")
     return p.parse_args()
@@ -248,25 +253,29 @@ def main():
     seed_cells = ps.original(ps.cell).cpu().numpy()
     period = ps.record_period(pathline=pathline)
     n_steps = cfg.n_steps
-    # launches: the whole run at N=1 (every launch re-reads the particle state and re-loads
-    # each particle's cell stencil: 30-step launches cost 6% at config 2); at N>1 quarters of
-    # the run, whose records are all-gathered while the next quarter computes, and a final
-    # one-record launch so that only one record's gather is exposed
-    seg = args.segment if args.segment > 0 else (n_steps if world == 1 else period * max(1, ps.K // 4))
+    # launches: the whole run as one segment (every launch re-reads the particle state and
+    # re-loads each particle's cell stencil: 30-step launches cost 6% at config 2); with
+    # --gather records at N>1, quarters of the run whose records are all-gathered while the next
+    # quarter computes, and a final one-record segment so that only one record's gather is exposed
+    gather_records = world > 1 and args.gather == "records"
+    seg = args.segment if args.segment > 0 else (period * max(1, ps.K // 4) if gather_records else n_steps)
     seg = max(period, (seg // period) * period)  # whole record periods per launch
     bounds = list(range(0, n_steps, seg)) + [n_steps]
-    if args.segment <= 0 and world > 1 and bounds[-1] - bounds[-2] > period:
+    if args.segment <= 0 and gather_records and bounds[-1] - bounds[-2] > period:
         bounds.insert(-1, bounds[-1] - period)
     segments = [(bounds[i], bounds[i + 1]) for i in range(len(bounds) - 1)]
     compute = torch.cuda.Stream(dev)
     comm = torch.cuda.Stream(dev)
     part_streams = [torch.cuda.Stream(dev) for _ in range(max(1, args.parts))]
-    gathered = gathered_ids = None
+    gathered = gathered_ids = ckpt = gathered_ckpt = None
     if world > 1:
-        # records are gathered in each rank's slot (locality) order, with the rank's slot -> particle
-        # ids once per call, so the gathered slabs map back to particles (distributed.unshard_slots)
-        gathered = torch.empty((ps.K, world, 6, n), dtype=torch.float64, device=dev)
+        # everything is gathered in each rank's slot (locality) order, with the rank's slot ->
+        # particle ids once per call, so it maps back to particles (distributed.unshard_slots)
         gathered_ids = torch.empty((world, n), dtype=torch.int32, device=dev)
+        ckpt = torch.empty((5, n), dtype=torch.float64, device=dev)  # x, y, z, depth, death step
+        gathered_ckpt = torch.empty((world, 5, n), dtype=torch.float64, device=dev)
+        if gather_records:
+            gathered = torch.empty((ps.K, world, 6, n), dtype=torch.float64, device=dev)
     seeds_dev = ps.seeds
 
     kernel_ms = []
@@ -291,14 +300,17 @@ def main():
                 e0.record(compute)
                 for st in part_streams:
                     st.wait_event(e0)
-                ps.advance_pipelined(dfield, dback, s0, s1, part_streams, args.chunks,
+                # step chunks in proportion to the segment's share of the run (N > 1 runs quarter
+                # segments whose record gathers overlap the next one: short launches cost ~6% each)
+                nch = max(1, round(args.chunks * (s1 - s0) / n_steps))
+                ps.advance_pipelined(dfield, dback, s0, s1, part_streams, nch,
                                      timing=dispatch_ms if timed else None)
                 for st in part_streams:
                     j = torch.cuda.Event(); j.record(st); compute.wait_event(j)
                 e1.record(compute)
                 if timed:
                     kernel_ms.append((e0, e1))
-                if world > 1:  # the records this segment completed, gathered while the next one computes
+                if gather_records:  # the records this segment completed, gathered while the next one computes
                     k0, k1 = s0 // period, min(s1 // period, ps.K)
                     if k1 > k0:
                         done = torch.cuda.Event()
@@ -307,6 +319,14 @@ def main():
                         with torch.cuda.stream(comm):
                             for k in range(k0, k1):
                                 all_gather_flat(dist, gathered[k].view(-1), ps.records[k].view(-1), args.backend)
+            if world > 1:  # the checkpoint: every particle's final state on every rank
+                ckpt[0].copy_(ps.x); ckpt[1].copy_(ps.y); ckpt[2].copy_(ps.z)
+                ckpt[3].copy_(ps.depth); ckpt[4].copy_(ps.death)
+                done = torch.cuda.Event()
+                done.record(compute)
+                comm.wait_event(done)
+                with torch.cuda.stream(comm):
+                    all_gather_flat(dist, gathered_ckpt.view(-1), ckpt.view(-1), args.backend)
         compute.synchronize()
         comm.synchronize()
 
@@ -350,7 +370,7 @@ def main():
                           f"ec30to60_{args.mode}_{args.method}_{args.particles}_seg{seg}_p{args.parts}c{args.chunks}",
                           per=f"segment ({args.parts} particle parts x {args.chunks} step chunks = "
                               f"{args.parts * args.chunks} overlapping traj_kernel launches)")
-    roof["dispatches_per_unit"] = len(dms) // max(1, args.steps * len(segments))
+    roof["dispatches_per_unit"] = len(dms) / max(1, args.steps * len(segments))
     roof["avg_dispatch_ms"] = (sum(dms) / len(dms)) if dms else None  # = rocprofv3's traj_kernel average
 
     cpu = None
@@ -384,8 +404,11 @@ def main():
                 "cells": mesh.nCells, "vertices": mesh.nVertices, "levels": mesh.nVertLevels,
                 "particles_per_gpu": n, "particles_total": int(n_all), "integration_steps": n_steps,
                 "records": ps.K, "method": args.method, "parallelism": f"particle-shard x{world}",
-                "record_gather": (f"{'rccl' if args.backend == 'nccl' else 'gloo'} all_gather per record instant "
-                                  "(side stream)") if world > 1 else "none",
+                "record_gather": ("none" if world == 1 else
+                                  f"{'rccl' if args.backend == 'nccl' else 'gloo'} all_gather of the final-state "
+                                  "checkpoint (+ slot ids) per call" + (
+                                      " and of every record slab, overlapped with the next quarter run"
+                                      if gather_records else "; records stay sharded on their rank")),
             },
             "nominal_particle_steps_per_call": n_all * n_steps,
             "attempted_particle_steps_per_call": attempted_all,
