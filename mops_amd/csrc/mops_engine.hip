@@ -83,6 +83,11 @@ struct mops_mesh {
     int origin_cell = -1;  // exact nearest centre to (0,0,0) (locate_kernel's tie rule)
     uint64_t* d_bkeys = nullptr;  // sorted bucket keys [C]
     int* d_bcells = nullptr;      // cell ids in key order [C]
+    // bucket directory: open-addressing hash table (load <= 1/2) from a non-empty bucket's
+    // key to its {first entry, entry count} in d_bkeys/d_bcells
+    uint64_t* d_hkeys = nullptr;  // [H] key or ~0 (empty)
+    int2* d_hval = nullptr;       // [H]
+    uint32_t hmask = 0;           // H - 1
     uint64_t* d_cell_key = nullptr;  // Morton key of each cell centre (particle locality order)
     double* d_cellB = nullptr;       // [C][maxv] Wachspress B_i of each cell polygon
     double* d_rloc2 = nullptr;       // [C] squared hinted-locate radius (locate_radius_kernel)
@@ -1418,13 +1423,55 @@ __global__ void bucket_keys_kernel(int64_t C, const double4* cxyz, double origin
     ids[i] = (int)i;
 }
 
-__device__ __forceinline__ int64_t lower_bound_u64(const uint64_t* a, int64_t n, uint64_t key) {
-    int64_t lo = 0, hi = n;
-    while (lo < hi) {
-        const int64_t mid = (lo + hi) >> 1;
-        if (a[mid] < key) lo = mid + 1; else hi = mid;
+// The seed-location bucket index: cells sorted by bucket key, plus a hash
+// directory from each non-empty bucket's key to its run of entries, so a
+// bucket costs one or two independent probes instead of an 18-step binary
+// search (27 per point in the first shell).
+struct BucketDir {
+    const uint64_t* keys;   // sorted bucket key per entry [C]
+    const int* ids;         // cell id per entry [C]
+    const uint64_t* hkeys;  // [hmask + 1] bucket key, or kEmptyKey
+    const int2* hval;       // {first entry, entry count}
+    uint32_t hmask;
+};
+constexpr uint64_t kEmptyKey = ~0ULL;  // bucket keys use 63 bits
+
+__device__ __forceinline__ uint32_t dir_hash(uint64_t k) {  // splitmix64 finaliser
+    k ^= k >> 30; k *= 0xbf58476d1ce4e5b9ULL;
+    k ^= k >> 27; k *= 0x94d049bb133111ebULL;
+    k ^= k >> 31;
+    return (uint32_t)k;
+}
+
+__device__ __forceinline__ int2 dir_find(const BucketDir& bd, uint64_t key) {
+    uint32_t slot = dir_hash(key) & bd.hmask;
+    for (;;) {  // terminates: the table is at most half full
+        const uint64_t k = bd.hkeys[slot];
+        if (k == key) return bd.hval[slot];
+        if (k == kEmptyKey) return make_int2(0, 0);
+        slot = (slot + 1) & bd.hmask;
     }
-    return lo;
+}
+
+// one thread per sorted entry; the first entry of each bucket's run inserts it
+__global__ void bucket_dir_kernel(int64_t C, const uint64_t* keys, uint64_t* hkeys, int2* hval, uint32_t hmask) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= C) return;
+    const uint64_t key = keys[i];
+    if (i > 0 && keys[i - 1] == key) return;
+    int64_t j = i + 1;
+    while (j < C && keys[j] == key) ++j;
+    uint32_t slot = dir_hash(key) & hmask;
+    for (;;) {
+        const unsigned long long prev =
+            atomicCAS(reinterpret_cast<unsigned long long*>(hkeys + slot), (unsigned long long)kEmptyKey,
+                      (unsigned long long)key);
+        if (prev == (unsigned long long)kEmptyKey) {
+            hval[slot] = make_int2((int)i, (int)(j - i));
+            return;
+        }
+        slot = (slot + 1) & hmask;
+    }
 }
 
 __device__ __forceinline__ void consider(const double4* cxyz, int cid, double qx, double qy, double qz, double& best,
@@ -1441,8 +1488,8 @@ __device__ __forceinline__ void consider(const double4* cxyz, int cid, double qx
 
 // Exact nearest cell centre to q (smallest id on ties), `exclude` skipped: bucket shells
 // around q until the best distance is provably final, else an exhaustive scan.
-__device__ int nearest_centre(double qx, double qy, double qz, int64_t C, const double4* cxyz, const uint64_t* keys,
-                              const int* ids, double origin, double h, int exclude, double& best,
+__device__ int nearest_centre(double qx, double qy, double qz, int64_t C, const double4* cxyz, const BucketDir& bd,
+                              double origin, double h, int exclude, double& best,
                               const int* excl = nullptr, int n_excl = 0) {
     best = INFINITY;
     int bi = -1;
@@ -1460,10 +1507,9 @@ __device__ int nearest_centre(double qx, double qy, double qz, int64_t C, const 
                         if (m != s) continue;
                         const int64_t ix = bx + dx, iy = by + dy, iz = bz + dz;
                         if (ix < 0 || iy < 0 || iz < 0 || ix >= kLim || iy >= kLim || iz >= kLim) continue;
-                        const uint64_t key = bkey(ix, iy, iz);
-                        int64_t j = lower_bound_u64(keys, C, key);
-                        for (; j < C && keys[j] == key; ++j)
-                            consider(cxyz, ids[j], qx, qy, qz, best, bi, exclude, excl, n_excl);
+                        const int2 run = dir_find(bd, bkey(ix, iy, iz));
+                        for (int j = run.x; j < run.x + run.y; ++j)
+                            consider(cxyz, bd.ids[j], qx, qy, qz, best, bi, exclude, excl, n_excl);
                     }
             // every point outside shells 0..s is at least s*h away
             const double bound = (double)s * h;
@@ -1488,8 +1534,8 @@ __device__ int nearest_centre(double qx, double qy, double qz, int64_t C, const 
 // at least ring(h) = the distance from h's centre to the nearest centre not in S away from
 // h's centre, hence at least ring(h) - |q - h| from q; if that exceeds the best distance
 // within S by a 1 m margin, the best of S (same tie rule) is the global answer.
-__global__ void locate_kernel(int64_t n, const double* pts, int64_t C, const double4* cxyz, const uint64_t* keys,
-                              const int* ids, double origin, double h, int origin_cell, const int* hint,
+__global__ void locate_kernel(int64_t n, const double* pts, int64_t C, const double4* cxyz, BucketDir bd,
+                              double origin, double h, int origin_cell, const int* hint,
                               const double* rloc2, const double* ring, const int* cellrec, int rec_ints,
                               int maxv, int* out) {
     const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -1522,13 +1568,13 @@ __global__ void locate_kernel(int64_t n, const double* pts, int64_t C, const dou
         }
     }
     double best;
-    out[i] = nearest_centre(qx, qy, qz, C, cxyz, keys, ids, origin, h, -1, best);
+    out[i] = nearest_centre(qx, qy, qz, C, cxyz, bd, origin, h, -1, best);
 }
 
 // rloc(c)^2 for the hinted locate: half the distance to the nearest other centre, shrunk
 // by 1e-9 relative and 1 m absolute (>> the rounding of |q - c| at Earth radius); -1 when
 // another centre coincides with c (never taken)
-__global__ void locate_radius_kernel(int64_t C, const double4* cxyz, const uint64_t* keys, const int* ids,
+__global__ void locate_radius_kernel(int64_t C, const double4* cxyz, BucketDir bd,
                                      double origin, double h, const int* cellrec, int rec_ints, int maxv,
                                      double* rloc2, double* ring) {
     const int64_t c = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -1540,11 +1586,11 @@ __global__ void locate_radius_kernel(int64_t C, const double4* cxyz, const uint6
         const int* r = cellrec + c * rec_ints;
         const int nv = min(r[0], maxv);
         double b2;
-        const int o = nearest_centre(p.x, p.y, p.z, C, cxyz, keys, ids, origin, h, (int)c, b2, r + 1 + maxv, nv);
+        const int o = nearest_centre(p.x, p.y, p.z, C, cxyz, bd, origin, h, (int)c, b2, r + 1 + maxv, nv);
         ring[c] = (o >= 0 && isfinite(b2)) ? sqrt(b2) * (1.0 - 1e-9) - 1.0 : -INFINITY;
     }
     double best;
-    const int nb = nearest_centre(p.x, p.y, p.z, C, cxyz, keys, ids, origin, h, (int)c, best);
+    const int nb = nearest_centre(p.x, p.y, p.z, C, cxyz, bd, origin, h, (int)c, best);
     double r2 = -1.0;
     if (nb < 0) {
         r2 = INFINITY;  // the only centre: every point's nearest
@@ -1756,7 +1802,7 @@ mops_status upload(const T* h, size_t count, T** d, int64_t* acc, hipStream_t s)
 void free_mesh(mops_mesh* m) {
     if (!m) return;
     (void)hipFree(m->d_cellrec); (void)hipFree(m->d_cxyz); (void)hipFree(m->d_vxyz); (void)hipFree(m->d_cov);
-    (void)hipFree(m->d_bkeys); (void)hipFree(m->d_bcells); (void)hipFree(m->d_cell_key); (void)hipFree(m->d_cellB); (void)hipFree(m->d_rloc2); (void)hipFree(m->d_ring);
+    (void)hipFree(m->d_bkeys); (void)hipFree(m->d_bcells); (void)hipFree(m->d_hkeys); (void)hipFree(m->d_hval); (void)hipFree(m->d_cell_key); (void)hipFree(m->d_cellB); (void)hipFree(m->d_rloc2); (void)hipFree(m->d_ring);
     (void)hipFree(m->d_scratch);
     delete m;
 }
@@ -1771,6 +1817,10 @@ void free_field(mops_field* f) {
 }
 
 }  // namespace
+
+BucketDir bucket_dir(const mops_mesh* m) {
+    return BucketDir{m->d_bkeys, m->d_bcells, m->d_hkeys, m->d_hval, m->hmask};
+}
 
 int64_t gcd64(int64_t a, int64_t b) {
     while (b) { int64_t t = a % b; a = b; b = t; }
@@ -1964,7 +2014,17 @@ mops_status mops_mesh_create(const mops_mesh_desc* desc, void* stream, mops_mesh
     cell_key_kernel<<<grid_for(C), kBlock, 0, s>>>(C, m->d_cxyz, m->d_cell_key);
     if ((st = dmalloc(&m->d_rloc2, (size_t)C, &acc)) != MOPS_OK) { free_mesh(m); return st; }
     if ((st = dmalloc(&m->d_ring, (size_t)C, &acc)) != MOPS_OK) { free_mesh(m); return st; }
-    locate_radius_kernel<<<grid_for(C), kBlock, 0, s>>>(C, m->d_cxyz, m->d_bkeys, m->d_bcells, m->bucket_origin,
+    {   // bucket directory (BucketDir): H = 2^k >= 2 C slots, so it is at most half full
+        uint32_t H = 2;
+        while ((int64_t)H < 2 * C) H <<= 1;
+        m->hmask = H - 1;
+        if ((st = dmalloc(&m->d_hkeys, (size_t)H, &acc)) != MOPS_OK ||
+            (st = dmalloc(&m->d_hval, (size_t)H, &acc)) != MOPS_OK) { free_mesh(m); return st; }
+        e = hipMemsetAsync(m->d_hkeys, 0xff, (size_t)H * sizeof(uint64_t), s);  // kEmptyKey
+        if (e != hipSuccess) { free_mesh(m); return fail(MOPS_ERR_HIP, hipGetErrorString(e)); }
+        bucket_dir_kernel<<<grid_for(C), kBlock, 0, s>>>(C, m->d_bkeys, m->d_hkeys, m->d_hval, m->hmask);
+    }
+    locate_radius_kernel<<<grid_for(C), kBlock, 0, s>>>(C, m->d_cxyz, bucket_dir(m), m->bucket_origin,
                                                         m->bucket_h, m->d_cellrec, m->rec_ints, m->maxv,
                                                         m->d_rloc2, m->d_ring);
     if ((st = dmalloc(&m->d_cellB, (size_t)(C * m->maxv), &acc)) != MOPS_OK) { free_mesh(m); return st; }
@@ -2182,7 +2242,7 @@ mops_status mops_locate_cells(const mops_mesh* mesh, int64_t n, const double* d_
         return fail(MOPS_ERR_INVALID, "mops_locate_cells: invalid argument");
     if (n == 0) return MOPS_OK;
     hipStream_t s = (hipStream_t)stream;
-    locate_kernel<<<grid_for(n), kBlock, 0, s>>>(n, d_points, mesh->C, mesh->d_cxyz, mesh->d_bkeys, mesh->d_bcells,
+    locate_kernel<<<grid_for(n), kBlock, 0, s>>>(n, d_points, mesh->C, mesh->d_cxyz, bucket_dir(mesh),
                                                  mesh->bucket_origin, mesh->bucket_h, mesh->origin_cell, nullptr,
                                                  nullptr, nullptr, nullptr, 0, 0, d_cells);
     HIP_TRY(hipGetLastError());
@@ -2195,7 +2255,7 @@ mops_status mops_locate_cells_hinted(const mops_mesh* mesh, int64_t n, const dou
         return fail(MOPS_ERR_INVALID, "mops_locate_cells_hinted: invalid argument");
     if (n == 0) return MOPS_OK;
     hipStream_t s = (hipStream_t)stream;
-    locate_kernel<<<grid_for(n), kBlock, 0, s>>>(n, d_points, mesh->C, mesh->d_cxyz, mesh->d_bkeys, mesh->d_bcells,
+    locate_kernel<<<grid_for(n), kBlock, 0, s>>>(n, d_points, mesh->C, mesh->d_cxyz, bucket_dir(mesh),
                                                  mesh->bucket_origin, mesh->bucket_h, mesh->origin_cell, d_hint,
                                                  mesh->d_rloc2, mesh->d_ring, mesh->d_cellrec, mesh->rec_ints,
                                                  mesh->maxv, d_cells);
