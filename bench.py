@@ -131,6 +131,30 @@ def engine_build_id() -> str:
     return h.hexdigest()[:16]
 
 
+PEAK_FP64_TFLOPS = 78.6  # MI355X FP64 vector (spec; half of the guide's 157.3 TF FP32 vector rate)
+
+
+def measured_entry(key: str):
+    """profiles/pmc_traffic.json's entry for this workload if it was measured on this engine build.
+    Returns (entry or None, provenance string)."""
+    pmc_path = os.path.join(ROOT, "profiles", "pmc_traffic.json")
+    if not os.path.exists(pmc_path):
+        return None, "no profiles/pmc_traffic.json"
+    try:
+        pm = json.load(open(pmc_path))
+    except (OSError, ValueError) as e:
+        return None, f"unreadable profiles/pmc_traffic.json: {e}"
+    bid = engine_build_id()
+    for e in (pm if isinstance(pm, list) else [pm]):
+        if e.get("workload") != key:
+            continue
+        if e.get("engine_build") != bid:
+            return None, f"stale: the PMC entry for {key} was measured on engine build {e.get('engine_build')}, not {bid}"
+        return e, (f"profiles/pmc_traffic.json[{key}] (rocprofv3 PMC passes per timed unit, engine build {bid}, "
+                   f"{e.get('profile', '?')})")
+    return None, f"no PMC entry for {key}"
+
+
 def measured_traffic(key: str):
     """Per-launch DRAM bytes of this workload from profiles/pmc_traffic.json (rocprofv3 FETCH_SIZE/WRITE_SIZE
     passes merged by tools/make_traffic.py), only if they were measured on this kernel build.
@@ -153,6 +177,18 @@ def measured_traffic(key: str):
     return None, f"no PMC entry for {key}"
 
 
+def fp64_block(key: str, unit_s: float):
+    """The FP64 vector-issue view of the same unit: PMC-counted FP64 add/mul/fma work over its time, against
+    the FP64 vector peak (the path's arithmetic is FP64 scalar geometry; no MFMA applies)."""
+    e, src = measured_entry(key)
+    fl = e.get("fp64_flops_per_unit") if e else None
+    if fl is None:
+        return {"achieved": None, "peak": PEAK_FP64_TFLOPS, "unit": "TFLOP/s", "frac": None, "source": src}
+    ach = fl / unit_s / 1e12
+    return {"achieved": ach, "peak": PEAK_FP64_TFLOPS, "unit": "TFLOP/s", "frac": ach / PEAK_FP64_TFLOPS,
+            "flops_per_unit": fl, "source": src + " SQ_INSTS_VALU_{ADD,MUL,FMA}_F64 x 64 lanes (fma = 2)"}
+
+
 def roofline_block(kernel: str, avg_kernel_s: float, psteps_per_launch: float, B: float, traffic_key: str,
                    per: str = "launch") -> dict:
     """The bench line's roofline: HBM GB/s MEASURED by rocprofv3 PMC counters (per launch) over the
@@ -172,6 +208,7 @@ def roofline_block(kernel: str, avg_kernel_s: float, psteps_per_launch: float, B
         "traffic_source": src,
         "limiter": ("not DRAM: dependent per-lane gathers (L1/TA-served) and FP64 VALU issue at 3 waves/SIMD "
                     "(DESIGN.md section 3)"),
+        "fp64_valu": fp64_block(traffic_key, avg_kernel_s),
         "kernel": kernel,
         "timed_unit": per,
         "particle_steps_per_launch": psteps_per_launch,

@@ -145,6 +145,32 @@ def test_bench_bytes_model():
     assert abs(bench.algorithmic_bytes_per_pstep(6, 80, 2) - 8844) < 50
 
 
+def test_bench_roofline_uses_only_this_builds_pmc(tmp_path):
+    """roofline.traffic/achieved/frac come from a PMC entry measured on this engine build only;
+    a stale or missing entry gives nulls (advisor finding: round 1 read the committed traffic
+    whatever kernel was built), and frac is a DRAM fraction, never the bytes model's."""
+    import importlib.util
+    import json
+    spec = importlib.util.spec_from_file_location("bench", os.path.join(ROOT, "bench.py"))
+    bench = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(bench)
+    (tmp_path / "profiles").mkdir()
+    key = "k"
+    bid = bench.engine_build_id()
+    bench.ROOT = str(tmp_path)
+    assert bench.roofline_block("kern", 0.03, 7.2e8, 3660.0, key)["traffic"] is None  # no file
+    pm = tmp_path / "profiles" / "pmc_traffic.json"
+    pm.write_text(json.dumps([{"workload": key, "engine_build": "0" * 16, "bytes_per_unit": 5e9}]))
+    r = bench.roofline_block("kern", 0.03, 7.2e8, 3660.0, key)
+    assert r["traffic"] is None and r["frac"] is None and "stale" in r["traffic_source"]
+    pm.write_text(json.dumps([{"workload": key, "engine_build": bid, "bytes_per_unit": 6e9,
+                               "fp64_flops_per_unit": 6.0e11}]))
+    r = bench.roofline_block("kern", 0.03, 7.2e8, 3660.0, key)
+    assert r["traffic"] == 6e9 and abs(r["achieved"] - 200.0) < 1e-9 and abs(r["frac"] - 0.025) < 1e-12
+    assert r["algorithmic_model"]["gbs"] > r["peak"]  # the model's rate is reported apart, not as frac
+    assert abs(r["fp64_valu"]["achieved"] - 20.0) < 1e-9
+
+
 # ---------------------------------------------------------------- gloo, world_size 2
 def _gloo_worker(rank, world, port, q):
     import torch.distributed as dist

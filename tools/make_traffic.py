@@ -23,6 +23,10 @@ def total(counter, d):
     v = [float(r["Counter_Value"]) for f in glob.glob(f"{out}/{d}/**/*counter_collection.csv", recursive=True)
          for r in csv.DictReader(open(f)) if "traj_kernel" in r["Kernel_Name"] and r["Counter_Name"] == counter]
     return sum(v), len(v)
+def total_any(counter):
+    v = [float(r["Counter_Value"]) for f in glob.glob(f"{out}/pmc/**/*counter_collection.csv", recursive=True)
+         for r in csv.DictReader(open(f)) if "traj_kernel" in r["Kernel_Name"] and r["Counter_Name"] == counter]
+    return sum(v), len(v)
 fetch, nf = total("FETCH_SIZE", "fetch")
 write, nw = total("WRITE_SIZE", "write")
 units = float(nf) if units_arg == "dispatches" else float(units_arg)
@@ -31,6 +35,13 @@ rec = dict(workload=workload, engine_build=bench.engine_build_id(), profile=labe
            bytes_per_unit=(2.0 * fetch + write) * 1024.0 / units,
            note="bytes_per_unit = (2*FETCH_SIZE + WRITE_SIZE)*1024 summed over the run's traj_kernel dispatches / units "
                 "(gfx950 FETCH_SIZE correction)")
+# FP64 VALU work of the same run (tools/profile_r02.sh's second counter pass), if present:
+# wave-instructions x 64 lanes, an FMA counted as 2 flops
+add, na = total_any("SQ_INSTS_VALU_ADD_F64")
+mul, nm = total_any("SQ_INSTS_VALU_MUL_F64")
+fma, nfm = total_any("SQ_INSTS_VALU_FMA_F64")
+if na and nm and nfm:
+    rec["fp64_flops_per_unit"] = 64.0 * (add + mul + 2.0 * fma) / units
 recs = []
 if os.path.exists(dst):
     old = json.load(open(dst))
