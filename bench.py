@@ -81,6 +81,9 @@ def parse():
                         "(position, depth, death) + slot ids -- particles are independent, so the path itself "
                         "needs no exchange and each rank keeps its shard's records; 'records' = all-gather every "
                         "record slab as well (1.15 GB per rank per call), overlapped with the next quarter run")
+    p.add_argument("--topography", choices=["sigma", "zlevel"], default="sigma",
+                   help="config 2: synthetic vertical grid (synth.make_snapshot): 'zlevel' = MPAS-O z-levels with "
+                        "partial bottom cells and zero-thickness inactive levels")
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--cpu-seconds", type=float, default=12.0, help="target CPU-baseline sample length")
     return p.parse_args()
@@ -277,11 +280,13 @@ def main():
         args.depth = layer_mid_depth(mesh, 10)
     if args.config in (3, 4, 5):
         return main_chain(args, mesh, dev, world, rank)
-    snap = synth.make_snapshot(mesh, timestep=0)
+    snap = synth.make_snapshot(mesh, timestep=0, topography=args.topography)
     dmesh = DeviceMesh.from_mesh(mesh)
     dfield = DeviceField.from_snapshot(dmesh, snap)
     pathline = args.mode == "pathline"
-    dback = DeviceField.from_snapshot(dmesh, synth.make_snapshot(mesh, timestep=1, phase=0.35)) if pathline else None
+    dback = (DeviceField.from_snapshot(dmesh, synth.make_snapshot(mesh, timestep=1, phase=0.35,
+                                                                  topography=args.topography))
+             if pathline else None)
     seeds = make_seeds(args.particles, rank)
     n = seeds.shape[0]
     cfg = TrajectoryConfig(deltaT=args.dt, simulationDuration=args.duration, recordT=args.record, depth=args.depth,
@@ -412,7 +417,8 @@ def main():
 
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        back_snap = synth.make_snapshot(mesh, timestep=1, phase=0.35) if pathline else None
+        back_snap = (synth.make_snapshot(mesh, timestep=1, phase=0.35, topography=args.topography)
+                     if pathline else None)
         cpu = cpu_baseline(mesh, snap, back_snap, seeds, seed_cells, args, n_steps)
 
     if os.environ.get("MOPS_PROF_SECTIONS") == "1":  # experiment builds (-DMOPS_PROF) only
@@ -441,6 +447,7 @@ def main():
                 "cells": mesh.nCells, "vertices": mesh.nVertices, "levels": mesh.nVertLevels,
                 "particles_per_gpu": n, "particles_total": int(n_all), "integration_steps": n_steps,
                 "records": ps.K, "method": args.method, "parallelism": f"particle-shard x{world}",
+                "topography": args.topography,
                 "record_gather": ("none" if world == 1 else
                                   f"{'rccl' if args.backend == 'nccl' else 'gloo'} all_gather of the final-state "
                                   "checkpoint (+ slot ids) per call" + (

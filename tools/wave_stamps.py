@@ -29,9 +29,10 @@ def main():
     torch.cuda.set_device(dev)
     mesh = synth.make_mesh(args.freq, n_levels=args.levels)
     dmesh = DeviceMesh.from_mesh(mesh)
-    dfield = DeviceField.from_snapshot(dmesh, synth.make_snapshot(mesh, timestep=0))
+    dfield = DeviceField.from_snapshot(dmesh, synth.make_snapshot(mesh, timestep=0, topography=args.topography))
     pathline = args.mode == "pathline"
-    dback = DeviceField.from_snapshot(dmesh, synth.make_snapshot(mesh, timestep=1, phase=0.35)) if pathline else None
+    dback = (DeviceField.from_snapshot(dmesh, synth.make_snapshot(mesh, timestep=1, phase=0.35, topography=args.topography))
+             if pathline else None)
     seeds = bench.make_seeds(args.particles, 0)
     n = seeds.shape[0]
     cfg = TrajectoryConfig(deltaT=args.dt, simulationDuration=args.duration, recordT=args.record, depth=args.depth,
