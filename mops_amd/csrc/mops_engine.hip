@@ -573,16 +573,22 @@ __device__ __forceinline__ int bracket_scan(const Cell<MAXV>& c, const double* w
 // = z_k there, computable level by level, and the bracket predicates are
 // monotone in the level everywhere (the fixed column is non-increasing by
 // construction).  a and b (see bracket_scan) are then found by walking from
-// the particle's previous layer (`hint`); typically two levels plus the
-// surface level are read instead of the whole column.  Any hint gives the
-// same result.  A walk that would need a level below km returns -2 (the
-// caller runs bracket_scan): below the prefix the fix-up may have fired.
+// the particle's previous layer (`hint`, clamped to km); typically two levels
+// plus the surface level are read instead of the whole column.  Any hint gives
+// the same result.  Below the prefix the fix-up may fire, so a walk towards the
+// bottom continues the reference's recurrence z'_k = z_k > z'_{k-1} ? z'_{k-1}
+// - 1e-9 : z_k from z'_{k-1} (exact: the chain starts inside the prefix, where
+// z' = z).  That keeps a partial-bottom column (flat zero-thickness layers under
+// the local bottom, km < L-1) off the whole-column scan for a particle sitting
+// below its bottom.  A NaN below the prefix (the column is no longer
+// non-increasing there) returns -2 and the caller runs bracket_scan, as does a
+// binary-search layer strictly inside (a, b) below the prefix.
 template <int MAXV, bool PATH>
 __device__ __forceinline__ int bracket_mono(const Cell<MAXV>& c, const double* w, const double* __restrict__ zt,
                                             int L, int km, double d, int& hint, double& zdn, double& zup) {
     const double eps = 1e-8;
-    int h = hint;
-    const bool hint_ok = (h >= 1 && h <= km);
+    int h = (hint > km) ? km : hint;
+    const bool hint_ok = (h >= 1);
     if (!hint_ok) h = 1;
     // one batch of independent loads: z_0, z_{h-1}, z_h (per-level sums keep
     // the reference's vertex order)
@@ -608,8 +614,7 @@ __device__ __forceinline__ int bracket_mono(const Cell<MAXV>& c, const double* w
             const int mid = (lo + hi) >> 1;
             if (d >= col<MAXV>(c, w, zt, L, mid) - eps) hi = mid; else lo = mid + 1;
         }
-        if (lo > km && km < L - 1) return -2;  // a lies below the prefix
-        h = (lo <= L - 1) ? lo : L - 1;
+        h = (lo <= km) ? lo : km;  // lo > km: a lies below the prefix, walk down from km
         zh = col<MAXV>(c, w, zt, L, h);
         zhm1 = (h == 1) ? z0 : col<MAXV>(c, w, zt, L, h - 1);
     }
@@ -630,13 +635,16 @@ __device__ __forceinline__ int bracket_mono(const Cell<MAXV>& c, const double* w
         double zk = zh, zprev = zh;
         bool found = false;
         while (k < L - 1) {
-            if (k >= km) return -2;
             ++k;
             zprev = zk;
             zk = col<MAXV>(c, w, zt, L, k);
+            if (k > km) {  // the reference's fix-up (a no-op inside the prefix)
+                if (isnan(zk)) return -2;
+                if (zk > zprev) zk = zprev - 1e-9;
+            }
             if (d >= zk - eps) { found = true; break; }
         }
-        if (!found) {  // Q(L-1) false  <=>  d < z_{L-1} - eps: the "below the bottom" branch (km = L-1 here)
+        if (!found) {  // Q(L-1) false  <=>  d < z'_{L-1} - eps: the "below the bottom" branch
             const double zlm1 = (k == h) ? zhm1 : zprev;
             zdn = zk; zup = zlm1; hint = L - 1;
             return L - 1;
@@ -648,8 +656,11 @@ __device__ __forceinline__ int bracket_mono(const Cell<MAXV>& c, const double* w
     int b = a;
     double zb = za, zbm1 = zam1;
     while (b < L - 1 && d <= zb + eps) {
-        if (b >= km) return -2;
-        const double zn = col<MAXV>(c, w, zt, L, b + 1);
+        double zn = col<MAXV>(c, w, zt, L, b + 1);
+        if (b + 1 > km) {
+            if (isnan(zn)) return -2;
+            if (zn > zb) zn = zb - 1e-9;
+        }
         zbm1 = zb; zb = zn; ++b;
     }
     int layer;
@@ -666,6 +677,7 @@ __device__ __forceinline__ int bracket_mono(const Cell<MAXV>& c, const double* w
     }
     if (layer == a) { zdn = za; zup = zam1; }
     else if (layer == b) { zdn = zb; zup = zbm1; }
+    else if (layer > km) return -2;  // strictly inside (a, b) below the prefix: needs the whole chain
     else { zdn = col<MAXV>(c, w, zt, L, layer); zup = col<MAXV>(c, w, zt, L, layer - 1); }
     hint = layer;
     return layer;

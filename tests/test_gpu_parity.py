@@ -469,8 +469,9 @@ def test_coastal_cells_boundary_vertices(dev_small, ref_small, small_case, oracl
 def test_zlevel_topography_partial_bottom(gpu, engine_lib, oracle_lib, method):
     """MPAS-O z-level columns: partial bottom cells and zero-thickness inactive levels
     make zTop columns end in flat runs, so each cell's fast bracket is limited to its
-    strictly decreasing prefix km (dev::fast_ok) and particles near or below the
-    local bottom fall back to the general bracket (bracket_mono returns -2).  Depths
+    strictly decreasing prefix km (dev::fast_ok); particles near or below the local
+    bottom walk below the prefix with the reference's fix-up chained level by level
+    (dev::bracket_mono), or fall back to the whole-column scan.  Depths
     span the surface, mid-column, the bottom region and below the deepest bottom."""
     from mops_amd import synth
     from mops_amd.engine import DeviceField, DeviceMesh, TrajectoryConfig, run_trajectories
