@@ -411,13 +411,31 @@ __device__ __forceinline__ void load_cell(Cell<MAXV>& c, int cell, const int* __
     }
 }
 
+// The cell's vertex count as the evaluation sees it: NV > 0 is a compile-time
+// count the caller has checked for every lane of the wave (eval_at), so the
+// per-slot `v < nv` masks and the polygon's wrap-around selects fold away;
+// NV = 0 reads it from the cell.
+#ifndef MOPS_HEX
+#define MOPS_HEX 1  // NV = 6 instantiation for all-hexagon waves
+#endif
+// ... and for the level-pair sums: pathline yes (measured -2%, PE/PR); streamline no --
+// without the per-vertex branch its scheduler spills (register-cached polygon), 2.4x slower
+#ifndef MOPS_HEX_PAIRS
+#define MOPS_HEX_PAIRS 0
+#endif
+#ifndef MOPS_HEX_PAIRS_P
+#define MOPS_HEX_PAIRS_P 1
+#endif
+template <int NV, int MAXV>
+__device__ __forceinline__ int nverts(const Cell<MAXV>& c) { return NV > 0 ? NV : c.nv; }
+
 // guards + TBBKernel::IsInMesh + Interpolator::CalcPolygonWachspress
 // (MPASOVisualizerKernels.cpp:744-770, TBBKernel.h:21-54, Interpolation.hpp:137-165)
-template <int MAXV>
+template <int MAXV, int NV>
 __device__ __forceinline__ bool weights(const Cell<MAXV>& c, int L, int V, double px, double py, double pz,
                                         double* w) {
     if (c.id < 0 || L <= 1 || L > kMaxLevels) return false;
-    const int nv = c.nv;
+    const int nv = nverts<NV>(c);
     if (nv <= 0 || nv > kMaxVertex) return false;
     if (!isfinite(px) || !isfinite(py) || !isfinite(pz)) return false;
     // rotated slots (see Cell): X[0] = poly[nv-1], X[j] = poly[j-1]
@@ -454,6 +472,7 @@ __device__ __forceinline__ bool weights(const Cell<MAXV>& c, int L, int V, doubl
             const double nz = X[i] * by - Y[i] * bx;
             inside = inside & !(nx * px + ny * py + nz * pz < 0.0);  // no short circuit: straight-line code
             w[i] = tri_area(X[i], Y[i], Z[i], bx, by, bz, px, py, pz);
+            if constexpr (NV > 0) __builtin_amdgcn_sched_barrier(0);  // one slot at a time (register pressure)
         } else {
             w[i] = 0.0;
         }
@@ -771,12 +790,12 @@ __device__ __forceinline__ int walk(Cell<MAXV>& c, int cell, double x, double y,
     return cell;
 }
 
-template <int MAXV>
+template <int MAXV, int NV>
 __device__ __forceinline__ bool weights_finite(const Cell<MAXV>& c, const double* w) {
     bool ok = true;
 #pragma unroll
     for (int i = 0; i < MAXV; ++i)
-        if (i < c.nv) ok = ok & isfinite(w[i]);
+        if (i < nverts<NV>(c)) ok = ok & isfinite(w[i]);
     return ok;
 }
 
@@ -797,7 +816,7 @@ __device__ __forceinline__ bool weights_finite(const Cell<MAXV>& c, const double
 // 0..km (drop - 2 * error >= W * (1e-6 - 4.8e-9)); W >= 1e-200 keeps every
 // term clear of subnormal rounding.  The reference's fix-up therefore never
 // fires there and its bracket predicates are monotone in the level.
-template <int MAXV>
+template <int MAXV, int NV>
 __device__ __forceinline__ int fast_ok(const Cell<MAXV>& c, uint32_t m, bool wfin, const double* w) {
     if (!(m & 0x80000000u) || !wfin) return -1;
     const int km = (int)((m >> 20) & 0x7fu);
@@ -806,7 +825,7 @@ __device__ __forceinline__ int fast_ok(const Cell<MAXV>& c, uint32_t m, bool wfi
     double W = 0.0;
 #pragma unroll
     for (int i = 0; i < MAXV; ++i)
-        if (i < c.nv && !((zmask >> i) & 1u)) W += w[i];
+        if (i < nverts<NV>(c) && !((zmask >> i) & 1u)) W += w[i];
     return (W >= 1e-200) ? km : -1;
 }
 
@@ -834,7 +853,7 @@ struct Pair {
 // +0.0 and only adds products is never -0.0 (x + -x = +0 under
 // round-to-nearest) and S + +0.0 == S otherwise (NaN, inf included), so
 // every sum keeps the bits of the reference's nv-term loop.
-template <int MAXV, int GR>
+template <int MAXV, int GR, int NV>
 __device__ __forceinline__ void pair_sums(const Cell<MAXV>& c, const double* w, const double* __restrict__ pr, int L,
                                           int k, Pair& S) {
     S.zm = S.zk = S.wm = S.wk = 0.0;
@@ -843,7 +862,7 @@ __device__ __forceinline__ void pair_sums(const Cell<MAXV>& c, const double* w, 
     const uint32_t zrec = (uint32_t)c.V * (uint32_t)(L - 1);
 #pragma unroll
     for (int v0 = 0; v0 < MAXV; v0 += GR) {
-        if (v0 < c.nv) {
+        if (v0 < nverts<NV>(c)) {
             double2 a[GR][kPairRec / 2];
 #pragma unroll
             for (int j = 0; j < GR; ++j) {
@@ -852,7 +871,7 @@ __device__ __forceinline__ void pair_sums(const Cell<MAXV>& c, const double* w, 
     #if defined(MOPS_ABL_PAIR1)
             const uint32_t ri = (uint32_t)c.vid[0] * (uint32_t)(L - 1) + (uint32_t)(k - 1);
 #else
-            const uint32_t ri = (v < c.nv) ? (uint32_t)c.vid[v] * (uint32_t)(L - 1) + (uint32_t)(k - 1) : zrec;
+            const uint32_t ri = (v < nverts<NV>(c)) ? (uint32_t)c.vid[v] * (uint32_t)(L - 1) + (uint32_t)(k - 1) : zrec;
 #endif
                 const double2* r = reinterpret_cast<const double2*>(pr + (uint64_t)ri * kPairRec);
 #pragma unroll
@@ -868,6 +887,9 @@ __device__ __forceinline__ void pair_sums(const Cell<MAXV>& c, const double* w, 
                 S.um0 += wv * a[j][2].x; S.um1 += wv * a[j][2].y; S.um2 += wv * a[j][3].x;
                 S.uk0 += wv * a[j][3].y; S.uk1 += wv * a[j][4].x; S.uk2 += wv * a[j][4].y;
             }
+            // NV > 0 has no per-group branch: keep the groups apart, or the
+            // scheduler puts every record in flight at once and spills
+            if constexpr (NV > 0) __builtin_amdgcn_sched_barrier(0);
         }
     }
 }
@@ -886,13 +908,13 @@ __device__ __forceinline__ void pair_sums(const Cell<MAXV>& c, const double* w, 
 // bottom" branch).  Otherwise bracket_mono walks from the hint inside the prefix,
 // and bracket_scan (the whole fixed-up column) runs when the walk would leave
 // it; the record of the final layer is then read.
-template <int MAXV, bool PATH, int GR>
+template <int MAXV, bool PATH, int GR, int NV>
 __device__ __forceinline__ int layer_eval(const Cell<MAXV>& c, const double* w, int km, const Field& f, int L,
                                           double d, int& hint, Pair& S) {
     const double eps = 1e-8;
     const int h = hint;
     if (h >= 1 && h <= km) {  // km = -1: general bracket only (fast_ok)
-        pair_sums<MAXV, GR>(c, w, f.pr, L, h, S);
+        pair_sums<MAXV, GR, NV>(c, w, f.pr, L, h, S);
         bool ok;
         if (h == 1 && d > S.zm + eps) {  // above the surface (z_0 = z_{h-1} here)
             ok = true;
@@ -918,21 +940,21 @@ __device__ __forceinline__ int layer_eval(const Cell<MAXV>& c, const double* w, 
         hint = layer;
     }
     if (layer < 0) return -1;
-    pair_sums<MAXV, GR>(c, w, f.pr, L, layer, S);
+    pair_sums<MAXV, GR, NV>(c, w, f.pr, L, layer, S);
     S.zk = zdn;  // the bracket's (possibly fixed-up) column values
     S.zm = zup;
     return layer;
 }
 
 // streamline calc_velocity_at (MPASOVisualizerKernels.cpp:740-872)
-template <int MAXV, int GR>
+template <int MAXV, int GR, int NV>
 __device__ __forceinline__ bool eval_stream(const Cell<MAXV>& c, int L, int V, const Field& f, double px, double py,
                                             double pz, double d, int& hint, double& hx, double& hy, double& hz,
                                             double& wv) {
     double w[MAXV];
-    if (!weights<MAXV>(c, L, V, px, py, pz, w)) return false;
+    if (!weights<MAXV, NV>(c, L, V, px, py, pz, w)) return false;
     Pair S;
-    const int layer = layer_eval<MAXV, false, GR>(c, w, fast_ok<MAXV>(c, c.mono0, weights_finite<MAXV>(c, w), w), f,
+    const int layer = layer_eval<MAXV, false, GR, MOPS_HEX_PAIRS ? NV : 0>(c, w, fast_ok<MAXV, NV>(c, c.mono0, weights_finite<MAXV, NV>(c, w), w), f,
                                                   L, d, hint, S);
     if (layer < 0) return false;
     const double zdn = S.zk, zup = S.zm;
@@ -954,16 +976,16 @@ __device__ __forceinline__ bool eval_stream(const Cell<MAXV>& c, int L, int V, c
 // pathline calc_velocity_at (MPASOVisualizerKernels.cpp:1124-1327).  The
 // attribute channel is not evaluated: FinalizeTrajectoryLinesWithAttrs never
 // reads it (TrajectoryCommon.h:176-185, quirk Q9), so it is unobservable.
-template <int MAXV, int GR>
+template <int MAXV, int GR, int NV>
 __device__ __forceinline__ bool eval_path(const Cell<MAXV>& c, int L, int V, const Field& ff, const Field& fb,
                                           double px, double py, double pz, double d, double alpha, int& hint0,
                                           int& hint1, double& hx, double& hy, double& hz, double& wv) {
     double w[MAXV];
-    if (!weights<MAXV>(c, L, V, px, py, pz, w)) return false;
-    const bool wfin = weights_finite<MAXV>(c, w);
+    if (!weights<MAXV, NV>(c, L, V, px, py, pz, w)) return false;
+    const bool wfin = weights_finite<MAXV, NV>(c, w);
     Pair F, B;
-    const int lf = layer_eval<MAXV, true, GR>(c, w, fast_ok<MAXV>(c, c.mono0, wfin, w), ff, L, d, hint0, F);
-    const int lb = layer_eval<MAXV, true, GR>(c, w, fast_ok<MAXV>(c, c.mono1, wfin, w), fb, L, d, hint1, B);
+    const int lf = layer_eval<MAXV, true, GR, MOPS_HEX_PAIRS_P ? NV : 0>(c, w, fast_ok<MAXV, NV>(c, c.mono0, wfin, w), ff, L, d, hint0, F);
+    const int lb = layer_eval<MAXV, true, GR, MOPS_HEX_PAIRS_P ? NV : 0>(c, w, fast_ok<MAXV, NV>(c, c.mono1, wfin, w), fb, L, d, hint1, B);
     if (lf < 0 || lb < 0) return false;
     const double xf = dmax(F.zk, dmin(d, F.zm));
     const double denf = F.zm - F.zk;
@@ -984,6 +1006,22 @@ __device__ __forceinline__ bool eval_path(const Cell<MAXV>& c, int L, int V, con
     const double wb = tb * B.wm + (1.0 - tb) * B.wk;
     wv = alpha * wb + (1.0 - alpha) * wf;
     return true;
+}
+
+// One velocity evaluation.  A wave whose lanes all sit in hexagons (the bulk
+// of an MPAS mesh) runs the NV = 6 instantiation; any other wave the general
+// one.  Both compute the same operations in the same order.
+template <int MAXV, bool PATH, int GR>
+__device__ __forceinline__ bool eval_at(bool hex, const Cell<MAXV>& c, int L, int V, const Field& f0,
+                                        const Field& f1, double px, double py, double pz, double d, double alpha,
+                                        int& hint0, int& hint1, double& hx, double& hy, double& hz, double& wv) {
+    if constexpr (MAXV == 7) {
+        if (hex)
+            return PATH ? eval_path<MAXV, GR, 6>(c, L, V, f0, f1, px, py, pz, d, alpha, hint0, hint1, hx, hy, hz, wv)
+                        : eval_stream<MAXV, GR, 6>(c, L, V, f0, px, py, pz, d, hint0, hx, hy, hz, wv);
+    }
+    return PATH ? eval_path<MAXV, GR, 0>(c, L, V, f0, f1, px, py, pz, d, alpha, hint0, hint1, hx, hy, hz, wv)
+                : eval_stream<MAXV, GR, 0>(c, L, V, f0, px, py, pz, d, hint0, hx, hy, hz, wv);
 }
 
 }  // namespace dev
@@ -1089,6 +1127,13 @@ __global__ void __launch_bounds__(kTrajBlock, (TrajWaves<MAXV, PATH, EULER>::val
     c.nv = 0;
     c.V = a.V;
     const int C = a.C;
+    // next recording step (the smallest j >= step_begin with (j+1) % rec_period == 0) and its
+    // record index, advanced by counting instead of a 64-bit modulo per step
+    int64_t rec_next = -1, rec_k = 0;
+    if (a.rec_period > 0) {
+        rec_k = a.step_begin / a.rec_period;
+        rec_next = (rec_k + 1) * a.rec_period - 1;
+    }
     for (int64_t step = a.step_begin; step < a.step_end; ++step) {
         if (step == 0) {  // first_loop (:892-901)
             if (cell < 0 || cell >= C) { died = 0; break; }
@@ -1133,12 +1178,12 @@ __global__ void __launch_bounds__(kTrajBlock, (TrajWaves<MAXV, PATH, EULER>::val
         }
         const double d = -1.0 * (double)dep;
         const double r = dev::len3(x, y, z);
+        const bool hex = MOPS_HEX && __all(c.nv == 6);  // wave-uniform (dev::eval_at)
         double hx = 0, hy = 0, hz = 0, wv = 0;
         double nx, ny, nz;
         const double alpha = PATH ? (double)step / (double)a.n_steps : 0.0;
         if (EULER) {
-            bool ok = PATH ? dev::eval_path<MAXV, PairGroup<PATH, EULER>::value>(c, a.L, a.V, a.f0, a.f1, x, y, z, d, alpha, hint0, hint1, hx, hy, hz, wv)
-                           : dev::eval_stream<MAXV, PairGroup<PATH, EULER>::value>(c, a.L, a.V, a.f0, x, y, z, d, hint0, hx, hy, hz, wv);
+            bool ok = dev::eval_at<MAXV, PATH, PairGroup<PATH, EULER>::value>(hex, c, a.L, a.V, a.f0, a.f1, x, y, z, d, alpha, hint0, hint1, hx, hy, hz, wv);
             if (!ok) { died = (int)step; break; }
             const double ax = y * hz - z * hy, ay = z * hx - x * hz, az = x * hy - y * hx;
             const double speed = dev::len3(hx, hy, hz);
@@ -1149,22 +1194,18 @@ __global__ void __launch_bounds__(kTrajBlock, (TrajWaves<MAXV, PATH, EULER>::val
             double s1x, s1y, s1z, s1w, s2x, s2y, s2z, s2w, s3x, s3y, s3z, s3w, s4x, s4y, s4z, s4w;
             double qx, qy, qz;
             const double a1 = alpha;
-            bool ok = PATH ? dev::eval_path<MAXV, PairGroup<PATH, EULER>::value>(c, a.L, a.V, a.f0, a.f1, x, y, z, d, a1, hint0, hint1, s1x, s1y, s1z, s1w)
-                           : dev::eval_stream<MAXV, PairGroup<PATH, EULER>::value>(c, a.L, a.V, a.f0, x, y, z, d, hint0, s1x, s1y, s1z, s1w);
+            bool ok = dev::eval_at<MAXV, PATH, PairGroup<PATH, EULER>::value>(hex, c, a.L, a.V, a.f0, a.f1, x, y, z, d, a1, hint0, hint1, s1x, s1y, s1z, s1w);
             if (!ok) { died = (int)step; break; }
             dev::advect((unsigned)step, x, y, z, s1x, s1y, s1z, dt * 0.5, qx, qy, qz);
             const double a2 = PATH ? dev::dclamp(a1 + 0.5 * a.dalpha, 0.0, 1.0) : 0.0;
-            ok = PATH ? dev::eval_path<MAXV, PairGroup<PATH, EULER>::value>(c, a.L, a.V, a.f0, a.f1, qx, qy, qz, d, a2, hint0, hint1, s2x, s2y, s2z, s2w)
-                      : dev::eval_stream<MAXV, PairGroup<PATH, EULER>::value>(c, a.L, a.V, a.f0, qx, qy, qz, d, hint0, s2x, s2y, s2z, s2w);
+            ok = dev::eval_at<MAXV, PATH, PairGroup<PATH, EULER>::value>(hex, c, a.L, a.V, a.f0, a.f1, qx, qy, qz, d, a2, hint0, hint1, s2x, s2y, s2z, s2w);
             if (!ok) { died = (int)step; break; }
             dev::advect((unsigned)step, x, y, z, s2x, s2y, s2z, dt * 0.5, qx, qy, qz);
-            ok = PATH ? dev::eval_path<MAXV, PairGroup<PATH, EULER>::value>(c, a.L, a.V, a.f0, a.f1, qx, qy, qz, d, a2, hint0, hint1, s3x, s3y, s3z, s3w)
-                      : dev::eval_stream<MAXV, PairGroup<PATH, EULER>::value>(c, a.L, a.V, a.f0, qx, qy, qz, d, hint0, s3x, s3y, s3z, s3w);
+            ok = dev::eval_at<MAXV, PATH, PairGroup<PATH, EULER>::value>(hex, c, a.L, a.V, a.f0, a.f1, qx, qy, qz, d, a2, hint0, hint1, s3x, s3y, s3z, s3w);
             if (!ok) { died = (int)step; break; }
             dev::advect((unsigned)step, x, y, z, s3x, s3y, s3z, dt, qx, qy, qz);
             const double a4 = PATH ? dev::dclamp(a1 + a.dalpha, 0.0, 1.0) : 0.0;
-            ok = PATH ? dev::eval_path<MAXV, PairGroup<PATH, EULER>::value>(c, a.L, a.V, a.f0, a.f1, qx, qy, qz, d, a4, hint0, hint1, s4x, s4y, s4z, s4w)
-                      : dev::eval_stream<MAXV, PairGroup<PATH, EULER>::value>(c, a.L, a.V, a.f0, qx, qy, qz, d, hint0, s4x, s4y, s4z, s4w);
+            ok = dev::eval_at<MAXV, PATH, PairGroup<PATH, EULER>::value>(hex, c, a.L, a.V, a.f0, a.f1, qx, qy, qz, d, a4, hint0, hint1, s4x, s4y, s4z, s4w);
             if (!ok) { died = (int)step; break; }
             // (s1 + 2 s2 + 2 s3 + s4) / 6 -- cy::Vec3 operator order (:959-960)
             hx = (((s1x + s2x * 2.0) + s3x * 2.0) + s4x) / 6.0;
@@ -1190,8 +1231,10 @@ __global__ void __launch_bounds__(kTrajBlock, (TrajWaves<MAXV, PATH, EULER>::val
             a.rec[5 * a.rec_stride + pid] = hz;
         }
         x = nx; y = ny; z = nz;
-        if (a.rec_period > 0 && ((step + 1) % a.rec_period) == 0) {
-            const int64_t k = (step + 1) / a.rec_period - 1;
+        if (step == rec_next) {  // (step + 1) % rec_period == 0, record k = (step + 1) / rec_period - 1
+            const int64_t k = rec_k;
+            rec_next += a.rec_period;
+            ++rec_k;
             if (k < a.K) {
                 double* rk = a.rec + k * 6 * a.rec_stride;
                 rk[0 * a.rec_stride + pid] = x;
