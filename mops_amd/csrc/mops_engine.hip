@@ -339,11 +339,15 @@ struct Cell {
     // poly[k], p) are the slot pair (k, k+1), wrapping to slot 0 only at k = nv-1
     double x[MAXV], y[MAXV], z[MAXV];
     double B[MAXV];  // Wachspress B_i = area(poly[i-1], poly[i], poly[i+1]) (depends on the polygon only)
+    bool lds_n;         // compile-time constant per kernel (load_cell<MAXV, RC, NRM>): nrm below is live
+    // lds_n: IsInMesh edge normals n_i = X_i x X_{i+1} (slot pairs as in dev::weights), computed
+    // by load_cell into this lane's LDS column: component j of slot i at nrm[(3 * i + j) * kTrajBlock]
+    double* nrm;
     const double4* __restrict__ vxyz;   // rc == false: polygon re-read per evaluation (L1-resident)
     const double* __restrict__ cellB;   // rc == false: per-cell B_i [C][MAXV] (cell_b_kernel)
 };
 
-template <int MAXV, bool RC>
+template <int MAXV, bool RC, bool NRM>
 __device__ __forceinline__ void load_cell(Cell<MAXV>& c, int cell, const int* __restrict__ cellrec,
                                           const double4* __restrict__ vxyz, const uint32_t* __restrict__ mono0,
                                           const uint32_t* __restrict__ mono1, const double4* __restrict__ cxyz,
@@ -366,6 +370,7 @@ __device__ __forceinline__ void load_cell(Cell<MAXV>& c, int cell, const int* __
     c.nv = buf[0];
     const int nv = c.nv;
     c.rc = RC;
+    c.lds_n = RC && NRM;
 #pragma unroll
     for (int k = 0; k < MAXV; ++k) c.vid[k] = buf[1 + k];
     c.vlast = 0;
@@ -405,6 +410,18 @@ __device__ __forceinline__ void load_cell(Cell<MAXV>& c, int cell, const int* __
         c.x[0] = lx; c.y[0] = ly; c.z[0] = lz;
 #pragma unroll
         for (int j = 1; j < MAXV; ++j) { c.x[j] = px[j - 1]; c.y[j] = py[j - 1]; c.z[j] = pz[j - 1]; }
+#pragma unroll
+        for (int i = 0; i < MAXV; ++i) {
+            if (NRM && i < nv) {
+                const bool wrap = (i + 1 >= nv);
+                const double bx = wrap ? c.x[0] : c.x[(i + 1) % MAXV];
+                const double by = wrap ? c.y[0] : c.y[(i + 1) % MAXV];
+                const double bz = wrap ? c.z[0] : c.z[(i + 1) % MAXV];
+                c.nrm[(3 * i + 0) * kTrajBlock] = c.y[i] * bz - c.z[i] * by;
+                c.nrm[(3 * i + 1) * kTrajBlock] = c.z[i] * bx - c.x[i] * bz;
+                c.nrm[(3 * i + 2) * kTrajBlock] = c.x[i] * by - c.y[i] * bx;
+            }
+        }
     } else {
         c.vxyz = vxyz;
         c.cellB = cellB;
@@ -467,9 +484,14 @@ __device__ __forceinline__ bool weights(const Cell<MAXV>& c, int L, int V, doubl
             const double bx = wrap ? X[0] : X[(i + 1) % MAXV];
             const double by = wrap ? Y[0] : Y[(i + 1) % MAXV];
             const double bz = wrap ? Z[0] : Z[(i + 1) % MAXV];
-            const double nx = Y[i] * bz - Z[i] * by;
-            const double ny = Z[i] * bx - X[i] * bz;
-            const double nz = X[i] * by - Y[i] * bx;
+            double nx, ny, nz;  // the edge normal X_i x X_{i+1}: cached per cell (load_cell) or computed
+            if (c.lds_n) {
+                nx = c.nrm[(3 * i + 0) * kTrajBlock]; ny = c.nrm[(3 * i + 1) * kTrajBlock]; nz = c.nrm[(3 * i + 2) * kTrajBlock];
+            } else {
+                nx = Y[i] * bz - Z[i] * by;
+                ny = Z[i] * bx - X[i] * bz;
+                nz = X[i] * by - Y[i] * bx;
+            }
             inside = inside & !(nx * px + ny * py + nz * pz < 0.0);  // no short circuit: straight-line code
             w[i] = tri_area(X[i], Y[i], Z[i], bx, by, bz, px, py, pz);
             if constexpr (NV > 0) __builtin_amdgcn_sched_barrier(0);  // one slot at a time (register pressure)
@@ -1088,6 +1110,17 @@ struct RCache {
     static constexpr bool value =
         MAXV <= 7 && (PATH ? (EULER ? MOPS_RC_PE : MOPS_RC_PR) : (EULER ? MOPS_RC_SE : MOPS_RC_SR));
 };
+// Edge normals of the register-cached polygon kept in LDS (10.5 KB per 64-lane
+// block) instead of recomputed per evaluation: streamline Euler only -- in
+// streamline RK4 the extra registers cross 256 VGPRs (1 wave per SIMD): measured
+// 27.9 vs 29.0 ms (SE) and 135 vs 92 ms (SR) at config 2.
+#ifndef MOPS_NRM_SE
+#define MOPS_NRM_SE 1
+#endif
+template <int MAXV, bool PATH, bool EULER>
+struct LdsNormals {
+    static constexpr bool value = RCache<MAXV, PATH, EULER>::value && !PATH && EULER && MOPS_NRM_SE;
+};
 template <int MAXV, bool PATH, bool EULER>
 struct TrajWaves {
     static constexpr int base = PATH ? (EULER ? MOPS_W_PE : MOPS_W_PR) : (EULER ? MOPS_W_SE : MOPS_W_SR);
@@ -1126,6 +1159,9 @@ __global__ void __launch_bounds__(kTrajBlock, (TrajWaves<MAXV, PATH, EULER>::val
     c.id = -1;
     c.nv = 0;
     c.V = a.V;
+    constexpr bool kRC = RCache<MAXV, PATH, EULER>::value, kNrm = LdsNormals<MAXV, PATH, EULER>::value;
+    __shared__ double s_nrm[kNrm ? 3 * MAXV * kTrajBlock : 1];  // per-lane edge normals (Cell::nrm)
+    c.nrm = s_nrm + threadIdx.x;
     const int C = a.C;
     // next recording step (the smallest j >= step_begin with (j+1) % rec_period == 0) and its
     // record index, advanced by counting instead of a 64-bit modulo per step
@@ -1137,14 +1173,14 @@ __global__ void __launch_bounds__(kTrajBlock, (TrajWaves<MAXV, PATH, EULER>::val
     for (int64_t step = a.step_begin; step < a.step_end; ++step) {
         if (step == 0) {  // first_loop (:892-901)
             if (cell < 0 || cell >= C) { died = 0; break; }
-            dev::load_cell<MAXV, RCache<MAXV, PATH, EULER>::value>(c, cell, a.cellrec, a.vxyz, a.mono0, a.mono1, a.cxyz, a.cellB);
+            dev::load_cell<MAXV, kRC, kNrm>(c, cell, a.cellrec, a.vxyz, a.mono0, a.mono1, a.cxyz, a.cellB);
             double* r0 = a.rec;
             r0[0 * a.rec_stride + pid] = x;
             r0[1 * a.rec_stride + pid] = y;
             r0[2 * a.rec_stride + pid] = z;
         } else {  // one-hop nearest-centre walk (:902-922)
             if (cell < 0 || cell >= C) { died = (int)step; break; }
-            if (c.id != cell) dev::load_cell<MAXV, RCache<MAXV, PATH, EULER>::value>(c, cell, a.cellrec, a.vxyz, a.mono0, a.mono1, a.cxyz, a.cellB);
+            if (c.id != cell) dev::load_cell<MAXV, kRC, kNrm>(c, cell, a.cellrec, a.vxyz, a.mono0, a.mono1, a.cxyz, a.cellB);
             // Exact shortcut: inside the stay ball around the anchor every
             // neighbour is strictly farther than c by more than rounding, so
             // the reference's argmin (c listed last, strict <) keeps c (dev::walk).
@@ -1155,7 +1191,7 @@ __global__ void __launch_bounds__(kTrajBlock, (TrajWaves<MAXV, PATH, EULER>::val
             if (walking) {
                 cell = dev::walk<MAXV>(c, cell, x, y, z, a.cellrec, a.cxyz, C);
                 loading = c.id != cell;
-                if (c.id != cell) dev::load_cell<MAXV, RCache<MAXV, PATH, EULER>::value>(c, cell, a.cellrec, a.vxyz, a.mono0, a.mono1, a.cxyz, a.cellB);
+                if (c.id != cell) dev::load_cell<MAXV, kRC, kNrm>(c, cell, a.cellrec, a.vxyz, a.mono0, a.mono1, a.cxyz, a.cellB);
             }
             {
                 const unsigned long long bw = __ballot(walking), bl = __ballot(loading), ba = __ballot(1);
@@ -1172,7 +1208,7 @@ __global__ void __launch_bounds__(kTrajBlock, (TrajWaves<MAXV, PATH, EULER>::val
             if (!(ex * ex + ey * ey + ez * ez < c.rs2)) {
                 cell = dev::walk<MAXV>(c, cell, x, y, z, a.cellrec, a.cxyz, C);
                 if (c.id != cell) MOPS_CNT(5, 1);
-                if (c.id != cell) dev::load_cell<MAXV, RCache<MAXV, PATH, EULER>::value>(c, cell, a.cellrec, a.vxyz, a.mono0, a.mono1, a.cxyz, a.cellB);
+                if (c.id != cell) dev::load_cell<MAXV, kRC, kNrm>(c, cell, a.cellrec, a.vxyz, a.mono0, a.mono1, a.cxyz, a.cellB);
             }
 #endif
         }
