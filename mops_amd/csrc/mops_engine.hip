@@ -370,14 +370,18 @@ __device__ __forceinline__ void load_cell(Cell<MAXV>& c, int cell, const int* __
     c.nv = buf[0];
     const int nv = c.nv;
     c.rc = RC;
-    c.lds_n = RC && NRM;
+    c.lds_n = NRM;
 #pragma unroll
     for (int k = 0; k < MAXV; ++k) c.vid[k] = buf[1 + k];
     c.vlast = 0;
 #pragma unroll
     for (int k = 0; k < MAXV; ++k)
         if (k == nv - 1) c.vlast = c.vid[k];
-    if constexpr (RC) {
+    if constexpr (!RC) {
+        c.vxyz = vxyz;
+        c.cellB = cellB;
+    }
+    if constexpr (RC || NRM) {
         double px[MAXV], py[MAXV], pz[MAXV];  // natural order
 #pragma unroll
         for (int k = 0; k < MAXV; ++k) {
@@ -392,39 +396,38 @@ __device__ __forceinline__ void load_cell(Cell<MAXV>& c, int cell, const int* __
 #pragma unroll
         for (int k = 0; k < MAXV; ++k)
             if (k == nv - 1) { lx = px[k]; ly = py[k]; lz = pz[k]; }
-#pragma unroll
-        for (int i = 0; i < MAXV; ++i) {
-            if (i < nv) {
-                const double qx = (i == 0) ? lx : px[(i + MAXV - 1) % MAXV];
-                const double qy = (i == 0) ? ly : py[(i + MAXV - 1) % MAXV];
-                const double qz = (i == 0) ? lz : pz[(i + MAXV - 1) % MAXV];
-                const bool wrap = (i + 1 >= nv);
-                const double nx = wrap ? px[0] : px[(i + 1) % MAXV];
-                const double ny = wrap ? py[0] : py[(i + 1) % MAXV];
-                const double nz = wrap ? pz[0] : pz[(i + 1) % MAXV];
-                c.B[i] = tri_area(qx, qy, qz, px[i], py[i], pz[i], nx, ny, nz);
-            } else {
-                c.B[i] = 0.0;
-            }
-        }
-        c.x[0] = lx; c.y[0] = ly; c.z[0] = lz;
-#pragma unroll
-        for (int j = 1; j < MAXV; ++j) { c.x[j] = px[j - 1]; c.y[j] = py[j - 1]; c.z[j] = pz[j - 1]; }
+        // edge normals: rotated slot pair i (see Cell) is (poly[i-1], poly[i]), poly[-1] = poly[nv-1]
 #pragma unroll
         for (int i = 0; i < MAXV; ++i) {
             if (NRM && i < nv) {
-                const bool wrap = (i + 1 >= nv);
-                const double bx = wrap ? c.x[0] : c.x[(i + 1) % MAXV];
-                const double by = wrap ? c.y[0] : c.y[(i + 1) % MAXV];
-                const double bz = wrap ? c.z[0] : c.z[(i + 1) % MAXV];
-                c.nrm[(3 * i + 0) * kTrajBlock] = c.y[i] * bz - c.z[i] * by;
-                c.nrm[(3 * i + 1) * kTrajBlock] = c.z[i] * bx - c.x[i] * bz;
-                c.nrm[(3 * i + 2) * kTrajBlock] = c.x[i] * by - c.y[i] * bx;
+                const double qx = (i == 0) ? lx : px[(i + MAXV - 1) % MAXV];
+                const double qy = (i == 0) ? ly : py[(i + MAXV - 1) % MAXV];
+                const double qz = (i == 0) ? lz : pz[(i + MAXV - 1) % MAXV];
+                c.nrm[(3 * i + 0) * kTrajBlock] = qy * pz[i] - qz * py[i];
+                c.nrm[(3 * i + 1) * kTrajBlock] = qz * px[i] - qx * pz[i];
+                c.nrm[(3 * i + 2) * kTrajBlock] = qx * py[i] - qy * px[i];
             }
         }
-    } else {
-        c.vxyz = vxyz;
-        c.cellB = cellB;
+        if constexpr (RC) {
+#pragma unroll
+            for (int i = 0; i < MAXV; ++i) {
+                if (i < nv) {
+                    const double qx = (i == 0) ? lx : px[(i + MAXV - 1) % MAXV];
+                    const double qy = (i == 0) ? ly : py[(i + MAXV - 1) % MAXV];
+                    const double qz = (i == 0) ? lz : pz[(i + MAXV - 1) % MAXV];
+                    const bool wrap = (i + 1 >= nv);
+                    const double nx = wrap ? px[0] : px[(i + 1) % MAXV];
+                    const double ny = wrap ? py[0] : py[(i + 1) % MAXV];
+                    const double nz = wrap ? pz[0] : pz[(i + 1) % MAXV];
+                    c.B[i] = tri_area(qx, qy, qz, px[i], py[i], pz[i], nx, ny, nz);
+                } else {
+                    c.B[i] = 0.0;
+                }
+            }
+            c.x[0] = lx; c.y[0] = ly; c.z[0] = lz;
+#pragma unroll
+            for (int j = 1; j < MAXV; ++j) { c.x[j] = px[j - 1]; c.y[j] = py[j - 1]; c.z[j] = pz[j - 1]; }
+        }
     }
 }
 
@@ -1110,16 +1113,19 @@ struct RCache {
     static constexpr bool value =
         MAXV <= 7 && (PATH ? (EULER ? MOPS_RC_PE : MOPS_RC_PR) : (EULER ? MOPS_RC_SE : MOPS_RC_SR));
 };
-// Edge normals of the register-cached polygon kept in LDS (10.5 KB per 64-lane
-// block) instead of recomputed per evaluation: streamline Euler only -- in
+// The polygon's IsInMesh edge normals kept in LDS (10.5 KB per 64-lane block),
+// computed at each cell change instead of per evaluation: Euler modes only -- in
 // streamline RK4 the extra registers cross 256 VGPRs (1 wave per SIMD): measured
 // 27.9 vs 29.0 ms (SE) and 135 vs 92 ms (SR) at config 2.
 #ifndef MOPS_NRM_SE
 #define MOPS_NRM_SE 1
 #endif
+#ifndef MOPS_NRM_PE
+#define MOPS_NRM_PE 1
+#endif
 template <int MAXV, bool PATH, bool EULER>
 struct LdsNormals {
-    static constexpr bool value = RCache<MAXV, PATH, EULER>::value && !PATH && EULER && MOPS_NRM_SE;
+    static constexpr bool value = MAXV <= 7 && EULER && (PATH ? MOPS_NRM_PE : MOPS_NRM_SE);
 };
 template <int MAXV, bool PATH, bool EULER>
 struct TrajWaves {
