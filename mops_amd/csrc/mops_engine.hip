@@ -878,6 +878,9 @@ struct Pair {
 // +0.0 and only adds products is never -0.0 (x + -x = +0 under
 // round-to-nearest) and S + +0.0 == S otherwise (NaN, inf included), so
 // every sum keeps the bits of the reference's nv-term loop.
+#ifndef MOPS_PAIR_BARRIER
+#define MOPS_PAIR_BARRIER 1
+#endif
 template <int MAXV, int GR, int NV>
 __device__ __forceinline__ void pair_sums(const Cell<MAXV>& c, const double* w, const double* __restrict__ pr, int L,
                                           int k, Pair& S) {
@@ -914,7 +917,7 @@ __device__ __forceinline__ void pair_sums(const Cell<MAXV>& c, const double* w, 
             }
             // NV > 0 has no per-group branch: keep the groups apart, or the
             // scheduler puts every record in flight at once and spills
-            if constexpr (NV > 0) __builtin_amdgcn_sched_barrier(0);
+            if constexpr (NV > 0 && MOPS_PAIR_BARRIER) __builtin_amdgcn_sched_barrier(0);
         }
     }
 }
@@ -1099,7 +1102,7 @@ struct TrajArgs {
 #define MOPS_GR_R 2  // RK4
 #endif
 #ifndef MOPS_GR_PE
-#define MOPS_GR_PE MOPS_GR_E  // pathline Euler
+#define MOPS_GR_PE 2  // pathline Euler (with the NV = 6 pair sums: 44.6 vs 45.7 ms at GR 1, config 2 mesh)
 #endif
 template <bool PATH, bool EULER>
 struct PairGroup {
