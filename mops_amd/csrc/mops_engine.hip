@@ -64,6 +64,9 @@ constexpr int kBlock = 256;
 #endif
 constexpr int kTrajBlock = MOPS_TRAJ_BLOCK;
 constexpr int kPairRec = 10;  // doubles per level-pair record (see mops_field::d_pr)
+#ifndef MOPS_PR_LEVEL_MAJOR
+#define MOPS_PR_LEVEL_MAJOR 1  // record (v, k) at index (k-1)*V + v (level-major; 0: v*(L-1) + k-1, vertex-major)
+#endif
 
 inline int rec_ints_for(int maxv) { return ((1 + 2 * maxv) + 3) / 4 * 4; }
 
@@ -899,7 +902,11 @@ __device__ __forceinline__ void pair_sums(const Cell<MAXV>& c, const double* w, 
     #if defined(MOPS_ABL_PAIR1)
             const uint32_t ri = (uint32_t)c.vid[0] * (uint32_t)(L - 1) + (uint32_t)(k - 1);
 #else
+#if MOPS_PR_LEVEL_MAJOR
+            const uint32_t ri = (v < nverts<NV>(c)) ? (uint32_t)(k - 1) * (uint32_t)c.V + (uint32_t)c.vid[v] : zrec;
+#else
             const uint32_t ri = (v < nverts<NV>(c)) ? (uint32_t)c.vid[v] * (uint32_t)(L - 1) + (uint32_t)(k - 1) : zrec;
+#endif
 #endif
                 const double2* r = reinterpret_cast<const double2*>(pr + (uint64_t)ri * kPairRec);
 #pragma unroll
@@ -1807,8 +1814,16 @@ __global__ void pair_record_kernel(int64_t V, int L, const double* __restrict__ 
     if ((int64_t)j >= V * (L - 1) * (kPairRec / 2)) return;
     const IDX rec = j / (IDX)(kPairRec / 2);
     const int q = (int)(j - rec * (IDX)(kPairRec / 2));
+#if MOPS_PR_LEVEL_MAJOR
+    const IDX vv = (IDX)V;
+    const IDX kk = rec / vv;
+    const IDX v = rec - kk * vv;
+    const int k = (int)kk + 1;
+    (void)lm1;
+#else
     const IDX v = rec / lm1;
     const int k = (int)(rec - v * lm1) + 1;
+#endif
     double2 val;
     if (q == 0) {
         const double* z = zt + (int64_t)v * L;
