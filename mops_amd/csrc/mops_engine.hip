@@ -1838,6 +1838,49 @@ __global__ void pair_record_kernel(int64_t V, int L, const double* __restrict__ 
     reinterpret_cast<double2*>(pr)[j] = val;
 }
 
+// Level-major records ((k-1)*V + v) from the vertex-major zt/vel/w arrays: a block stages a
+// tile of kRecTV vertices x (kRecTK + 1) levels through LDS (reads run along each vertex's
+// column) and writes kRecTK rows of kRecTV consecutive records (contiguous 5 KB per row), so
+// both sides are coalesced.  Same values and chunk layout as pair_record_kernel.
+constexpr int kRecTV = 64, kRecTK = 16;
+__global__ void __launch_bounds__(256) pair_record_tiled_kernel(int64_t V, int L, const double* __restrict__ zt,
+                                                                const double* __restrict__ vel,
+                                                                const double* __restrict__ w,
+                                                                double* __restrict__ pr) {
+    __shared__ double sz[kRecTV][kRecTK + 1], sw[kRecTV][kRecTK + 1], su[kRecTV][kRecTK + 1][3];
+    const int64_t v0 = (int64_t)blockIdx.x * kRecTV;
+    const int k0 = (int)blockIdx.y * kRecTK;  // rows k-1 = k0 .. k0+nk-1 use levels k0 .. k0+nk
+    const int nk = min(kRecTK, L - 1 - k0);
+    const int nv = (int)min<int64_t>(kRecTV, V - v0);
+    const int t = (int)threadIdx.x;
+    for (int i = t; i < kRecTV * (kRecTK + 1); i += blockDim.x) {
+        const int vl = i / (kRecTK + 1), kl = i - vl * (kRecTK + 1);
+        if (vl < nv && kl <= nk) {
+            const int64_t v = v0 + vl;
+            sz[vl][kl] = zt[v * L + k0 + kl];
+            sw[vl][kl] = w[v * (L + 1) + k0 + kl];
+        }
+    }
+    for (int i = t; i < kRecTV * (kRecTK + 1) * 3; i += blockDim.x) {
+        const int vl = i / ((kRecTK + 1) * 3), r = i - vl * ((kRecTK + 1) * 3), kl = r / 3;
+        if (vl < nv && kl <= nk) su[vl][kl][r - kl * 3] = vel[((v0 + vl) * L + k0) * 3 + r];
+    }
+    __syncthreads();
+    for (int i = t; i < nk * kRecTV * (kPairRec / 2); i += blockDim.x) {
+        const int rl = i / (kPairRec / 2), q = i - rl * (kPairRec / 2);
+        const int kl = rl / kRecTV, vl = rl - kl * kRecTV;
+        if (vl >= nv) continue;
+        double2 val;
+        if (q == 0) val = make_double2(sz[vl][kl], sz[vl][kl + 1]);
+        else if (q == 1) val = make_double2(sw[vl][kl], sw[vl][kl + 1]);
+        else if (q == 2) val = make_double2(su[vl][kl][0], su[vl][kl][1]);
+        else if (q == 3) val = make_double2(su[vl][kl][2], su[vl][kl + 1][0]);
+        else val = make_double2(su[vl][kl + 1][1], su[vl][kl + 1][2]);
+        const int64_t rec = (int64_t)(k0 + kl) * V + v0 + vl;
+        reinterpret_cast<double2*>(pr)[rec * (kPairRec / 2) + q] = val;
+    }
+}
+
 __device__ __forceinline__ uint64_t spread3(uint64_t v) {  // 21 bits -> every third bit
     v &= 0x1fffffULL;
     v = (v | (v << 32)) & 0x1f00000000ffffULL;
@@ -2164,6 +2207,12 @@ static mops_status compute_mono(const mops_mesh* mesh, mops_field* f, hipStream_
     // + one all-zero record at index npr: pair_sums reads it for v >= nv
     if (!f->d_pr) MOPS_TRY(dmalloc(&f->d_pr, (size_t)((npr + 1) * kPairRec), &f->bytes));
     HIP_TRY(hipMemsetAsync(f->d_pr + npr * kPairRec, 0, kPairRec * sizeof(double), s));
+#if MOPS_PR_LEVEL_MAJOR
+    if (npr > 0) {
+        const dim3 grid((unsigned)((mesh->V + kRecTV - 1) / kRecTV), (unsigned)((mesh->L - 1 + kRecTK - 1) / kRecTK));
+        pair_record_tiled_kernel<<<grid, 256, 0, s>>>(mesh->V, mesh->L, f->d_zt, f->d_vel, f->d_w, f->d_pr);
+    }
+#else
     if (npr > 0)
     {
         const int64_t chunks = npr * (kPairRec / 2);
@@ -2174,6 +2223,7 @@ static mops_status compute_mono(const mops_mesh* mesh, mops_field* f, hipStream_
             pair_record_kernel<uint64_t><<<grid_for(chunks), kBlock, 0, s>>>(mesh->V, mesh->L, f->d_zt, f->d_vel,
                                                                            f->d_w, f->d_pr);
     }
+#endif
     if (!f->d_mono) MOPS_TRY(dmalloc(&f->d_mono, (size_t)mesh->C, &f->bytes));
     if (!f->d_vmono) MOPS_TRY(dmalloc(&f->d_vmono, (size_t)mesh->V, &f->bytes));
     if (!f->d_vzero) MOPS_TRY(dmalloc(&f->d_vzero, (size_t)mesh->V, &f->bytes));
