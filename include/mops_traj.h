@@ -100,7 +100,9 @@ int32_t mops_abi_version(void);
 /* Self-test of the trajectory kernel's exact math helpers on the device (not
  * a reference entry point): for n doubles at d_x, op 0 writes {fast sqrt,
  * sqrt()} pairs, op 1 writes {fast sin, sin(), fast cos, cos()} (|x| < 0.78
- * only; other x copy the library values) into d_out (2n or 4n doubles). */
+ * only; other x copy the library values) into d_out (2n or 4n doubles); op 2
+ * reads n 3-vectors (3n doubles) and writes {fast a_j / |a| (j = 0..2), a_j / |a|}
+ * (6n doubles; zeros where |a| <= 1e-12). */
 mops_status mops_selftest_math(int64_t n, const double* d_x, double* d_out, int32_t op, void* stream);
 
 /* ---- mesh / snapshots -------------------------------------------------- */

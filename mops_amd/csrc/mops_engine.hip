@@ -251,6 +251,42 @@ __device__ __forceinline__ double xdiv(double a, double b) { return a / b; }
 __device__ __forceinline__ double sq3(double x, double y, double z) { return x * x + y * y + z * z; }
 __device__ __forceinline__ double len3(double x, double y, double z) { return xsqrt(sq3(x, y, z)); }
 
+// q_j = a_j / b for the components of a vector and its length b = len3(a0, a1, a2)
+// (b > 1e-12 checked by the caller), bit-identical to three `/`.  gfx950's
+// correctly rounded a / b is div_scale(b), div_scale(a), rcp + two Newton steps
+// on the scaled b, q = a*r, e = fma(-b, q, a), div_fmas(e, r, q), div_fixup.
+// For b <= 2^300 and |a_j| >= 2^-700 no operand is scaled (b and 1/b normal,
+// exponent(a) - exponent(b) <= 1 since |a_j| <= b (1 + 2^-52), a/b >=
+// 2^-1000 normal, |a| >= 2^-969), so div_scale returns its input, div_fmas is
+// a plain fma and div_fixup returns the finite nonzero quotient unchanged: the
+// same operations on the same operands.  The reciprocal refinement depends on
+// b alone, so it is done once for the three quotients (5 instead of 3 x 11
+// instructions, one rcp instead of three).  Other operands (zero, tiny,
+// NaN/inf) take `/`.  Checked bitwise against `/` (mops_selftest_math op 2).
+#ifndef MOPS_FAST_DIV3
+#define MOPS_FAST_DIV3 1
+#endif
+__device__ __forceinline__ void xdiv_norm3(double a0, double a1, double a2, double b, double& q0, double& q1,
+                                           double& q2) {
+#if MOPS_FAST_DIV3 && !defined(MOPS_ABL_DIV)
+    if (__builtin_expect(b <= 0x1p300 && fabs(a0) >= 0x1p-700 && fabs(a1) >= 0x1p-700 && fabs(a2) >= 0x1p-700, 1)) {
+        double r = __builtin_amdgcn_rcp(b);
+        double e = __builtin_fma(-b, r, 1.0);
+        r = __builtin_fma(r, e, r);
+        e = __builtin_fma(-b, r, 1.0);
+        r = __builtin_fma(r, e, r);
+        double q = a0 * r;
+        q0 = __builtin_fma(__builtin_fma(-b, q, a0), r, q);
+        q = a1 * r;
+        q1 = __builtin_fma(__builtin_fma(-b, q, a1), r, q);
+        q = a2 * r;
+        q2 = __builtin_fma(__builtin_fma(-b, q, a2), r, q);
+        return;
+    }
+#endif
+    q0 = xdiv(a0, b); q1 = xdiv(a1, b); q2 = xdiv(a2, b);
+}
+
 // The reference's `length(v) < 1e-12` tests (MPASOVisualizerKernels.cpp:841-852)
 // without the square root: correctly rounded sqrt is monotone, and the
 // smallest double s with sqrt(s) >= 1e-12 is exactly the double 1e-24
@@ -289,7 +325,8 @@ __device__ __forceinline__ void rotate(unsigned salt, double px, double py, doub
 #endif
     const double al = len3(ax, ay, az);
     if (al <= 1e-12) { rx = px; ry = py; rz = pz; return; }
-    const double ux = xdiv(ax, al), uy = xdiv(ay, al), uz = xdiv(az, al);
+    double ux, uy, uz;
+    xdiv_norm3(ax, ay, az, al, ux, uy, uz);
     rx = (c + ux * ux * (1.0 - c)) * px + (ux * uy * (1.0 - c) - uz * s) * py + (ux * uz * (1.0 - c) + uy * s) * pz;
     ry = (uy * ux * (1.0 - c) + uz * s) * px + (c + uy * uy * (1.0 - c)) * py + (uy * uz * (1.0 - c) - ux * s) * pz;
     rz = (uz * ux * (1.0 - c) - uy * s) * px + (uz * uy * (1.0 - c) + ux * s) * py + (c + uz * uz * (1.0 - c)) * pz;
@@ -1094,7 +1131,7 @@ struct TrajArgs {
 #define MOPS_W_SE 3  // streamline Euler
 #endif
 #ifndef MOPS_W_SR
-#define MOPS_W_SR 1  // streamline RK4
+#define MOPS_W_SR 2  // streamline RK4 (at 1 the shared-reciprocal normalisation took it to 260 VGPRs = 1 wave)
 #endif
 #ifndef MOPS_W_PE
 #define MOPS_W_PE 3  // pathline Euler (at 1 the compiler takes 172 VGPRs = 2 waves: -9.5% at config 2's mesh)
@@ -1124,18 +1161,26 @@ struct RCache {
         MAXV <= 7 && (PATH ? (EULER ? MOPS_RC_PE : MOPS_RC_PR) : (EULER ? MOPS_RC_SE : MOPS_RC_SR));
 };
 // The polygon's IsInMesh edge normals kept in LDS (10.5 KB per 64-lane block),
-// computed at each cell change instead of per evaluation: Euler modes only -- in
-// streamline RK4 the extra registers cross 256 VGPRs (1 wave per SIMD): measured
-// 27.9 vs 29.0 ms (SE) and 135 vs 92 ms (SR) at config 2.
+// computed at each cell change instead of per evaluation: 27.9 vs 29.0 ms (SE)
+// at config 2.  In streamline RK4 the extra registers first crossed 256 VGPRs
+// (1 wave per SIMD, 135 vs 92 ms); with the RK4 kernels held at 2 waves/SIMD by
+// their launch bounds (MOPS_W_SR 2) they fit, and all four modes use them.
 #ifndef MOPS_NRM_SE
 #define MOPS_NRM_SE 1
 #endif
 #ifndef MOPS_NRM_PE
 #define MOPS_NRM_PE 1
 #endif
+#ifndef MOPS_NRM_SR
+#define MOPS_NRM_SR 1  // with MOPS_W_SR 2 capping it at 256 VGPRs: 86.3-87.0 vs 88.6-89.2 ms (config-2 mesh)
+#endif
+#ifndef MOPS_NRM_PR
+#define MOPS_NRM_PR 1  // 125.7 vs 127.2 ms
+#endif
 template <int MAXV, bool PATH, bool EULER>
 struct LdsNormals {
-    static constexpr bool value = MAXV <= 7 && EULER && (PATH ? MOPS_NRM_PE : MOPS_NRM_SE);
+    static constexpr bool value =
+        MAXV <= 7 && (EULER ? (PATH ? MOPS_NRM_PE : MOPS_NRM_SE) : (PATH ? MOPS_NRM_PR : MOPS_NRM_SR));
 };
 template <int MAXV, bool PATH, bool EULER>
 struct TrajWaves {
@@ -1266,7 +1311,10 @@ __global__ void __launch_bounds__(kTrajBlock, (TrajWaves<MAXV, PATH, EULER>::val
             wv = (s1w + 2.0 * s2w + 2.0 * s3w + s4w) / 6.0;
             const double tx = x + hx * dt, ty = y + hy * dt, tz = z + hz * dt;
             const double tl = dev::len3(tx, ty, tz);
-            if (tl > 1e-12) { nx = (tx / tl) * r; ny = (ty / tl) * r; nz = (tz / tl) * r; }
+            if (tl > 1e-12) {
+                dev::xdiv_norm3(tx, ty, tz, tl, nx, ny, nz);
+                nx *= r; ny *= r; nz *= r;
+            }
             else { nx = x; ny = y; nz = z; }
         }
         // vertical update (:977-986)
@@ -1276,7 +1324,10 @@ __global__ void __launch_bounds__(kTrajBlock, (TrajWaves<MAXV, PATH, EULER>::val
         const double r_new = dev::dmax(1.0, r + wv * (double)a.delta_t);
         dep = (float)nd;
         const double nl = dev::len3(nx, ny, nz);
-        if (nl > 1e-12) { nx = dev::xdiv(nx, nl) * r_new; ny = dev::xdiv(ny, nl) * r_new; nz = dev::xdiv(nz, nl) * r_new; }
+        if (nl > 1e-12) {
+            dev::xdiv_norm3(nx, ny, nz, nl, nx, ny, nz);
+            nx *= r_new; ny *= r_new; nz *= r_new;
+        }
         if (step == 0) {  // first_vel (:988-991)
             a.rec[3 * a.rec_stride + pid] = hx;
             a.rec[4 * a.rec_stride + pid] = hy;
@@ -1308,6 +1359,17 @@ __global__ void __launch_bounds__(kTrajBlock, (TrajWaves<MAXV, PATH, EULER>::val
 __global__ void selftest_math_kernel(int64_t n, const double* __restrict__ x, double* __restrict__ out, int op) {
     const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n) return;
+    if (op == 2) {  // x = n vectors (3 doubles each); out = 3 fast + 3 library quotients by their length
+        const double a0 = x[3 * i], a1 = x[3 * i + 1], a2 = x[3 * i + 2];
+        const double b = dev::len3(a0, a1, a2);
+        double q0 = 0.0, q1 = 0.0, q2 = 0.0;
+        if (b > 1e-12) dev::xdiv_norm3(a0, a1, a2, b, q0, q1, q2);
+        out[6 * i] = q0; out[6 * i + 1] = q1; out[6 * i + 2] = q2;
+        out[6 * i + 3] = b > 1e-12 ? a0 / b : 0.0;
+        out[6 * i + 4] = b > 1e-12 ? a1 / b : 0.0;
+        out[6 * i + 5] = b > 1e-12 ? a2 / b : 0.0;
+        return;
+    }
     const double v = x[i];
     if (op == 0) {
         out[2 * i] = dev::xsqrt(v);
@@ -2030,7 +2092,7 @@ int mops_debug_stamps(unsigned long long* d_buf, long long cap, int* occ) {
 int32_t mops_abi_version(void) { return MOPS_ABI_VERSION; }
 
 mops_status mops_selftest_math(int64_t n, const double* d_x, double* d_out, int32_t op, void* stream) {
-    if (n < 0 || (n > 0 && (!d_x || !d_out)) || (op != 0 && op != 1))
+    if (n < 0 || (n > 0 && (!d_x || !d_out)) || (op != 0 && op != 1 && op != 2))
         return fail(MOPS_ERR_INVALID, "mops_selftest_math: bad arguments");
     if (n == 0) return MOPS_OK;
     selftest_math_kernel<<<grid_for(n), kBlock, 0, (hipStream_t)stream>>>(n, d_x, d_out, op);

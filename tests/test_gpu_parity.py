@@ -97,6 +97,27 @@ def test_fast_math_helpers_match_library(gpu, engine_lib):
     assert np.array_equal(o[:, 0].view(np.int64), o[:, 1].view(np.int64)), "fast sin != sin()"
     assert np.array_equal(o[:, 2].view(np.int64), o[:, 3].view(np.int64)), "fast cos != cos()"
     print(f"device sin == host sin: {np.mean(o[:, 1] == np.sin(th)):.6f}, cos: {np.mean(o[:, 3] == np.cos(th)):.6f}")
+    # shared-reciprocal normalisation a / |a| (dev::xdiv_norm3) against three `/`, including
+    # zero, signed-zero, subnormal, huge and non-finite components
+    n = 600000
+    sgn = np.sign(rng.uniform(-1, 1, (n, 3)))
+    mags = np.concatenate([10.0 ** rng.uniform(-320, 308, (n // 3, 3)),            # any exponents
+                           10.0 ** rng.uniform(-230, -200, (n // 6, 3)),           # near the 2^-700 bound
+                           10.0 ** rng.uniform(88, 92, (n // 6, 3)),               # near the 2^300 bound
+                           rng.uniform(0, 6.4e6, (n - n // 3 - 2 * (n // 6), 3))])  # trajectory-sized
+    a = sgn * mags
+    a[rng.uniform(size=(n, 3)) < 0.03] = 0.0
+    a[rng.uniform(size=(n, 3)) < 0.01] = -0.0
+    special = np.array([[0.0, 0.0, 1.0], [-0.0, 1.0, 1.0], [5e-324, 1.0, 0.0], [np.inf, 1.0, 1.0], [np.nan, 1.0, 1.0],
+                        [2.0 ** -700, 1.0, 1.0], [np.nextafter(2.0 ** -700, 0), 1.0, 1.0], [2.0 ** 300, 0.0, 0.0],
+                        [2.0 ** 300, 2.0 ** 300, 0.0], [1e-13, 0.0, 0.0], [1e-12, 1e-12, 1e-12]])
+    a = np.concatenate([a, special])
+    d = torch.as_tensor(a.reshape(-1), device=gpu)
+    out = torch.empty((len(a), 6), dtype=torch.float64, device=gpu)
+    assert engine_lib.mops_selftest_math(len(a), ctypes.c_void_p(d.data_ptr()), ctypes.c_void_p(out.data_ptr()), 2,
+                                         None) == 0
+    o = out.cpu().numpy()
+    assert np.array_equal(o[:, :3].view(np.int64), o[:, 3:].view(np.int64)), "xdiv_norm3 != a / |a|"
 
 
 def test_preprocessing_bitwise(dev_small, ref_small, small_case):
