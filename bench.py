@@ -84,6 +84,10 @@ def parse():
     p.add_argument("--topography", choices=["sigma", "zlevel"], default="sigma",
                    help="config 2: synthetic vertical grid (synth.make_snapshot): 'zlevel' = MPAS-O z-levels with "
                         "partial bottom cells and zero-thickness inactive levels")
+    p.add_argument("--side-cus", type=int, default=0,
+                   help="configs 4/5: CUs reserved for a side stream that generates and derives snapshot p+2 while "
+                        "pair p computes on the others (three field buffers); 0 = off (two buffers, derivation "
+                        "between pairs, the default: measured slower, DESIGN.md section 3.3)")
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--cpu-seconds", type=float, default=12.0, help="target CPU-baseline sample length")
     return p.parse_args()
@@ -491,13 +495,23 @@ def main_chain(args, mesh, dev, world, rank):
         from mops_amd.synth_device import DeviceFieldRecycler, DeviceSnapshotSource
         src = DeviceSnapshotSource(mesh, dev)
         recycler = DeviceFieldRecycler(dmesh, src)
-        # the two field buffers are allocated before the timed region (hipMalloc of ~2 x 75 GB is
-        # setup); every snapshot a call uses is still generated and derived inside it
-        for i in range(2):
-            recycler.release(recycler(i, torch.cuda.current_stream(dev).cuda_stream))
+        side_cus = args.side_cus or 0
+        overlap = None
+        if side_cus > 0 and n_snap > 2:
+            from mops_amd.chain import cu_split_streams
+            compute_masked, overlap = cu_split_streams(dev, side_cus)
+            recycler.side = overlap  # snapshot generation runs there too
+        # the field buffers (2, or 3 with the overlap stream) are allocated before the timed region
+        # (hipMalloc of ~75 GB each is setup); every snapshot a call uses is still generated and
+        # derived inside it
+        bufs = [recycler(i, torch.cuda.current_stream(dev).cuda_stream) for i in range(3 if overlap else 2)]
+        for b in bufs:
+            recycler.release(b)
+        del bufs
         torch.cuda.synchronize()
         chain = PathlineChain(dmesh, recycler, n_snap, gap_seconds=args.duration,
-                              device=dev, own_fields=True, prefetch=False)
+                              device=dev, own_fields=True, prefetch=False, overlap_stream=overlap)
+        chain.overlap_stream_cus = side_cus
     if args.config == 4:  # strong scaling: 1e7 particles in total, one contiguous shard per rank
         allseeds = make_seeds(args.particles, 0)
         lo, hi = len(allseeds) * rank // world, len(allseeds) * (rank + 1) // world
@@ -509,6 +523,8 @@ def main_chain(args, mesh, dev, world, rank):
         seeds = make_seeds(args.particles, rank)
     n = seeds.shape[0]
     compute = torch.cuda.Stream(dev)
+    if args.config in (4, 5) and chain.overlap_stream is not None:
+        compute = compute_masked  # the trajectory launches leave the side stream's CUs free
     comm = torch.cuda.Stream(dev)
     n_pad = n
     if world > 1:  # equal-size all-gather buffers (config-4 shards may differ by one particle)
@@ -606,6 +622,8 @@ def main_chain(args, mesh, dev, world, rank):
                 "particles_per_gpu": n, "particles_total": int(n_all), "integration_steps": n_steps,
                 "records_per_pair": args.duration // args.record, "method": args.method,
                 "parallelism": f"particle-shard x{world}",
+                "snapshot_overlap": (f"snapshot p+2 generated + derived on a {chain.overlap_stream_cus}-CU side stream "
+                                     "during pair p (3 field buffers)") if chain.overlap_stream is not None else "none",
                 "record_gather": (f"{'rccl' if args.backend == 'nccl' else 'gloo'} all_gather of continuation points "
                                   "per pair") if world > 1 else "none"},
             "nominal_particle_steps_per_call": n_all * n_steps,

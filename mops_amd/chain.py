@@ -33,7 +33,7 @@ REORDER_SECONDS = 3 * 86400  # default launch length of long pairs (simulated ti
 
 class PathlineChain:
     def __init__(self, mesh: DeviceMesh, make_field, n_snapshots: int, gap_seconds: int, device=None,
-                 own_fields: bool = True, prefetch: bool = True):
+                 own_fields: bool = True, prefetch: bool = True, overlap_stream=None):
         """``make_field(i, stream) -> DeviceField`` builds snapshot i's field on ``stream``.
         With ``own_fields`` False the fields are the caller's (e.g. all resident
         before a timed region) and are neither freed nor rebuilt here.
@@ -43,7 +43,12 @@ class PathlineChain:
         Without prefetch, a ``make_field`` with ``refill(field, i, stream)``
         (and optionally ``prepare(i)``, e.g. synth_device.DeviceFieldRecycler)
         re-derives snapshot p's buffers in place as p+2 instead -- no
-        allocation and no host synchronisation between pairs."""
+        allocation and no host synchronisation between pairs.
+        ``overlap_stream`` (with such a recycling ``make_field`` holding three
+        field buffers): snapshot p+2 is generated and derived into the buffer
+        pair p-1 released, on that stream while pair p computes -- give it CUs
+        of its own (``cu_split_streams``): the trajectory waves fill every CU
+        they may use, so a stream sharing them only runs once they drain."""
         if n_snapshots < 2:
             raise ValueError("a pathline chain needs at least two snapshots")
         self.mesh = mesh
@@ -53,6 +58,7 @@ class PathlineChain:
         self.device = device
         self.own_fields = own_fields
         self.prefetch = prefetch
+        self.overlap_stream = overlap_stream
 
     def run(self, seeds, depth: float, particle_depths=None, method: int = L.MOPS_EULER, delta_t: int = 60,
             record_t: int = 360, direction: int = L.MOPS_FORWARD, follow_last: bool = True, keep_lines: bool = True,
@@ -96,9 +102,23 @@ class PathlineChain:
         last = None
         attempted = torch.zeros((), dtype=torch.int64, device=dev)
         recycle = self.own_fields and not self.prefetch and hasattr(self.make_field, "refill")
+        overlap = recycle and self.overlap_stream is not None
+        ov = self.overlap_stream
+        ready, pair_done = {}, {}
         for p in range(self.n_snapshots - 1):
-            if recycle and p + 2 < self.n_snapshots and hasattr(self.make_field, "prepare"):
+            if overlap and p + 2 < self.n_snapshots:
+                # snapshot p+2 into the buffer pair p-1 released (pair 0: the third pooled buffer)
+                buf = self.make_field.pool.pop() if p == 0 else fields.pop(p - 1)
+                if p > 0:
+                    ov.wait_event(pair_done.pop(p - 1))
+                with torch.cuda.stream(ov):
+                    fields[p + 2] = self.make_field.refill(buf, p + 2, ov)
+                    ready[p + 2] = torch.cuda.Event()
+                    ready[p + 2].record(ov)
+            elif recycle and p + 2 < self.n_snapshots and hasattr(self.make_field, "prepare"):
                 self.make_field.prepare(p + 2)  # raw snapshot p+2 generated on a side stream during pair p
+            if p + 1 in ready:
+                cs.wait_event(ready.pop(p + 1))  # pair p's back snapshot was derived on the overlap stream
             with torch.cuda.stream(cs):
                 if p == 0 or not follow_last:
                     s = seeds0
@@ -139,6 +159,10 @@ class PathlineChain:
                     tmp_acc.append(out["temperature"][:, sl]); sal_acc.append(out["salinity"][:, sl])
             if on_pair is not None:
                 on_pair(p, last)
+            if overlap:
+                pair_done[p] = torch.cuda.Event()
+                pair_done[p].record(cs)  # snapshot p's buffer is free once pair p has run
+                continue
             if recycle:  # re-derive snapshot p's buffers as snapshot p+2, stream-ordered after pair p
                 if p + 2 < self.n_snapshots:
                     fields[p + 2] = self.make_field.refill(fields.pop(p), p + 2, cs)
@@ -160,6 +184,8 @@ class PathlineChain:
                         fields[p + 2] = self.make_field(p + 2, cs.cuda_stream)
         if self.own_fields:
             cs.synchronize()
+            if ov is not None:
+                ov.synchronize()
             for f in fields.values():
                 if hasattr(self.make_field, "release"):
                     self.make_field.release(f)  # kept for the next run (e.g. DeviceFieldRecycler)
@@ -173,6 +199,41 @@ class PathlineChain:
         if cs != torch.cuda.current_stream(dev):
             torch.cuda.current_stream(dev).wait_stream(cs)  # results are read on the caller's stream
         return res
+
+
+def cu_split_streams(device, side_cus: int):
+    """(compute, side): two HIP streams that partition the device's CUs
+    (hipExtStreamCreateWithCUMask), ``side_cus`` of them for the side stream.
+    The side CUs are bits k*(n_cu/side_cus + 1) mod n_cu, which put one on each
+    XCD whether the mask's bits map to XCDs in contiguous blocks or round-robin
+    (256 CUs, 8 side CUs: bits 0, 33, 66, ...).  The streams live until exit."""
+    import ctypes as C
+    import torch
+    dev = torch.device(device)
+    n_cu = torch.cuda.get_device_properties(dev).multi_processor_count
+    if not (0 < side_cus < n_cu):
+        raise ValueError("side_cus must leave CUs on both sides")
+    stride = n_cu // side_cus + 1
+    side_bits = {(k * stride) % n_cu for k in range(side_cus)}
+    if len(side_bits) != side_cus:
+        side_bits = set(range(side_cus))
+    words = (n_cu + 31) // 32
+    lib = L.load()  # its hipExtStreamCreateWithCUMask is the HIP runtime torch uses (see _lib.load)
+    lib.hipExtStreamCreateWithCUMask.argtypes = [C.POINTER(C.c_void_p), C.c_uint32, C.POINTER(C.c_uint32)]
+    lib.hipExtStreamCreateWithCUMask.restype = C.c_int
+    out = []
+    for mine in (lambda b: b not in side_bits, lambda b: b in side_bits):
+        mask = (C.c_uint32 * words)()
+        for b in range(n_cu):
+            if mine(b):
+                mask[b // 32] |= 1 << (b % 32)
+        h = C.c_void_p()
+        with torch.cuda.device(dev):
+            rc = lib.hipExtStreamCreateWithCUMask(C.byref(h), words, mask)
+        if rc != 0:
+            raise RuntimeError(f"hipExtStreamCreateWithCUMask failed ({rc})")
+        out.append(torch.cuda.ExternalStream(h.value, device=dev))
+    return out[0], out[1]
 
 
 def snapshot_field_factory(mesh: DeviceMesh, make_snapshot):

@@ -101,3 +101,39 @@ def test_device_snapshot_generator_matches_host(engine_lib, gpu, small_case):
         b = getattr(h, k)
         assert a.shape == b.shape, k
         assert np.allclose(a, b, rtol=1e-12, atol=1e-15), k
+
+
+@pytest.mark.gpu
+def test_chain_overlap_stream_matches_serial(engine_lib, gpu, small_case):
+    """Config 4's schedule: snapshot p+2 generated and derived into the buffer pair
+    p-1 released, on a side stream with CUs of its own (cu_split_streams) while
+    pair p computes on the rest -- the same lines as the two-buffer chain that
+    derives between pairs."""
+    import torch
+    from mops_amd import synth
+    from mops_amd.chain import PathlineChain, cu_split_streams
+    from mops_amd.engine import DeviceMesh
+    from mops_amd.synth_device import DeviceFieldRecycler, DeviceSnapshotSource
+    mesh, _, _ = small_case
+    dm = DeviceMesh.from_mesh(mesh)
+    seeds = synth.uniform_band_seeds(150, seed=11)
+    n_snap = 6
+    results = []
+    for overlap in (False, True):
+        rec = DeviceFieldRecycler(dm, DeviceSnapshotSource(mesh, "cuda"))
+        compute, side = cu_split_streams("cuda", 8) if overlap else (torch.cuda.Stream(), None)
+        if overlap:
+            rec.side = side
+        cs = torch.cuda.current_stream().cuda_stream
+        bufs = [rec(i, cs) for i in range(3 if overlap else 2)]
+        for b in bufs:
+            rec.release(b)
+        torch.cuda.synchronize()
+        chain = PathlineChain(dm, rec, n_snap, gap_seconds=21600, prefetch=False, overlap_stream=side)
+        for _ in range(2):  # a second call reuses the pooled buffers
+            got = chain.run(seeds, depth=250.0, method=1, delta_t=600, record_t=3600, compute_stream=compute)
+        torch.cuda.synchronize()
+        results.append({k: got[k].cpu().numpy() for k in ("points", "velocity", "lastPoint")})
+        assert len(rec.pool) == (3 if overlap else 2)
+    for k in results[0]:
+        assert np.array_equal(results[0][k], results[1][k]), k
