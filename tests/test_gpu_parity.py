@@ -351,7 +351,7 @@ def test_order_is_permutation_and_result_invariant(gpu, dev_small, small_case):
     assert torch.equal(lc["points"], lb["points"]) and torch.equal(lc["velocity"], lb["velocity"])
 
 
-@pytest.mark.parametrize("max_edges", [10, 16])
+@pytest.mark.parametrize("max_edges", [10, 16, 20])
 def test_wide_stencil_instantiations(gpu, engine_lib, oracle_lib, max_edges):
     """maxEdges > 7 selects the MAXV 12 / 20 kernels (no register polygon
     cache, fewer waves); results must not depend on the padding width."""
@@ -372,6 +372,37 @@ def test_wide_stencil_instantiations(gpu, engine_lib, oracle_lib, max_edges):
                                  euler=(method == 1), cells=got["cells"])
             assert_lines_match(got, ref, f"maxEdges={max_edges} path={back is not None} method={method}")
             assert np.array_equal(got["points"], ref["points"])
+
+
+@pytest.mark.parametrize("levels", [2, 100, 101])
+def test_level_count_bounds(gpu, engine_lib, oracle_lib, levels):
+    """nVertLevels at the reference's bounds (MPASOVisualizerKernels.cpp:744-751:
+    1 < L <= MAX_VERTICAL_LEVEL_NUM = 100): L = 2 (a single layer) and L = 100
+    bit-exact against the oracle at depths through the whole column; L = 101 is
+    refused per particle, so every line dies at step 0 as in the reference."""
+    from mops_amd import synth
+    from mops_amd.engine import DeviceField, DeviceMesh, TrajectoryConfig, run_trajectories
+    mesh = synth.make_mesh(16, n_levels=levels)
+    s0 = synth.make_snapshot(mesh, timestep=0)
+    s1 = synth.make_snapshot(mesh, timestep=1, phase=0.35)
+    dm = DeviceMesh.from_mesh(mesh)
+    f0, f1 = DeviceField.from_snapshot(dm, s0), DeviceField.from_snapshot(dm, s1)
+    r0, r1 = oracle_lib.preprocess(mesh, s0), oracle_lib.preprocess(mesh, s1)
+    seeds = synth.uniform_band_seeds(200, seed=43)
+    depths = np.random.default_rng(5).uniform(-50.0, 4500.0, len(seeds)).astype(np.float32)
+    for back, rb in ((None, None), (f1, r1)):
+        for method in (1, 0):
+            cfg = TrajectoryConfig(deltaT=300, simulationDuration=21600, recordT=3600, depth=0.0, method=method)
+            got = run_trajectories(dm, f0, back, cfg, seeds, depths=depths)
+            ref = oracle_lib.run(mesh, r0, rb, seeds, depths=depths, delta_t=300, duration=21600, record_t=3600,
+                                 euler=(method == 1), cells=got["cells"])
+            label = f"L={levels} path={back is not None} method={method}"
+            assert_lines_match(got, ref, label)
+            assert np.array_equal(got["points"], ref["points"]), label
+            if levels > 100:
+                assert np.all(got["death_step"] == 0), label
+            else:
+                assert np.mean(got["death_step"] < 0) > 0.5, label
 
 
 def test_edge_case_seeds(dev_small, ref_small, small_case, oracle_lib):
