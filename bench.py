@@ -322,23 +322,24 @@ def main():
         gathered_ckpt = torch.empty((world, 5, n), dtype=torch.float64, device=dev)
         if gather_records:
             gathered = torch.empty((ps.K, world, 6, n), dtype=torch.float64, device=dev)
-    seeds_dev = ps.seeds
 
     kernel_ms = []
     dispatch_ms = []  # per traj_kernel launch (HIP events on its part stream): what rocprofv3 averages
 
-    def one_call(timed: bool):
-        """One StreamLine call on this rank's shard (device resident)."""
+    def one_call(timed: bool, pset=None):
+        """One StreamLine call on this rank's shard (device resident); ``pset``: another ParticleSet
+        of the same seeds (the RK4 companion line)."""
+        ps_ = pset if pset is not None else ps
         with torch.cuda.stream(compute):
-            ps.reset(depth=args.depth)
-            dmesh.locate(seeds_dev.data_ptr(), ps.cell.data_ptr(), n, stream=compute)
-            ps.reorder(stream=compute)
+            ps_.reset(depth=args.depth)
+            dmesh.locate(ps_.seeds.data_ptr(), ps_.cell.data_ptr(), n, stream=compute)  # seeds in slot order
+            ps_.reorder(stream=compute)
             if world > 1:
                 sorted_ev = torch.cuda.Event()
                 sorted_ev.record(compute)
                 comm.wait_event(sorted_ev)
                 with torch.cuda.stream(comm):
-                    all_gather_flat(dist, gathered_ids.view(-1), ps.ids, args.backend)
+                    all_gather_flat(dist, gathered_ids.view(-1), ps_.ids, args.backend)
             for (s0, s1) in segments:
                 # the segment's trajectory launches: particle parts on their own streams, each in
                 # step chunks, so one part's final partial round of waves overlaps the others' work
@@ -349,7 +350,7 @@ def main():
                 # step chunks in proportion to the segment's share of the run (N > 1 runs quarter
                 # segments whose record gathers overlap the next one: short launches cost ~6% each)
                 nch = max(1, round(args.chunks * (s1 - s0) / n_steps))
-                ps.advance_pipelined(dfield, dback, s0, s1, part_streams, nch,
+                ps_.advance_pipelined(dfield, dback, s0, s1, part_streams, nch,
                                      timing=dispatch_ms if timed else None)
                 for st in part_streams:
                     j = torch.cuda.Event(); j.record(st); compute.wait_event(j)
@@ -357,17 +358,17 @@ def main():
                 if timed:
                     kernel_ms.append((e0, e1))
                 if gather_records:  # the records this segment completed, gathered while the next one computes
-                    k0, k1 = s0 // period, min(s1 // period, ps.K)
+                    k0, k1 = s0 // period, min(s1 // period, ps_.K)
                     if k1 > k0:
                         done = torch.cuda.Event()
                         done.record(compute)
                         comm.wait_event(done)
                         with torch.cuda.stream(comm):
                             for k in range(k0, k1):
-                                all_gather_flat(dist, gathered[k].view(-1), ps.records[k].view(-1), args.backend)
+                                all_gather_flat(dist, gathered[k].view(-1), ps_.records[k].view(-1), args.backend)
             if world > 1:  # the checkpoint: every particle's final state on every rank
-                ckpt[0].copy_(ps.x); ckpt[1].copy_(ps.y); ckpt[2].copy_(ps.z)
-                ckpt[3].copy_(ps.depth); ckpt[4].copy_(ps.death)
+                ckpt[0].copy_(ps_.x); ckpt[1].copy_(ps_.y); ckpt[2].copy_(ps_.z)
+                ckpt[3].copy_(ps_.depth); ckpt[4].copy_(ps_.death)
                 done = torch.cuda.Event()
                 done.record(compute)
                 comm.wait_event(done)
@@ -394,6 +395,27 @@ def main():
     death = ps.death.to(torch.int64)
     attempted = torch.where(death < 0, torch.full_like(death, n_steps), death + 1).sum().item()
     dead = int((death >= 0).sum().item())
+    # the north star's integrator on the same workload, timed after the Euler line (N = 1 only;
+    # not part of `value`, which is the reference's default integrator, MPASOVisualizer.h:99)
+    rk4 = None
+    if world == 1 and args.method == "euler" and not pathline and os.environ.get("MOPS_BENCH_NO_RK4") != "1":
+        cfg4 = TrajectoryConfig(deltaT=args.dt, simulationDuration=args.duration, recordT=args.record,
+                                depth=args.depth, method=0)
+        ps4 = ParticleSet(dmesh, seeds, args.depth, cfg4, device=dev)
+        torch.cuda.synchronize()  # its locate + locality order ran on the current stream, not `compute`
+        one_call(False, ps4)
+        torch.cuda.synchronize()
+        t4 = time.perf_counter()
+        one_call(False, ps4)
+        torch.cuda.synchronize()
+        el4 = time.perf_counter() - t4
+        d4 = ps4.death.to(torch.int64)
+        att4 = torch.where(d4 < 0, torch.full_like(d4, n_steps), d4 + 1).sum().item()
+        rk4 = {"value": att4 / el4, "unit": "particle-steps/s", "ms_per_call": el4 * 1e3,
+               "dead_fraction": float((d4 >= 0).sum().item()) / max(n, 1),
+               "note": "same workload integrated with RK4 (four evaluations per step in the step's start "
+                       "cell, quirk Q1), one timed call after the Euler line; not part of value"}
+        del ps4
     kms = [a.elapsed_time(b) for (a, b) in kernel_ms]
     avg_kernel_s = (sum(kms) / len(kms)) / 1e3 if kms else float("nan")
     dms = [a.elapsed_time(b) for (a, b) in dispatch_ms]
@@ -464,6 +486,8 @@ def main():
             "roofline": roof,
             "cpu_baseline": cpu,
         }
+        if rk4 is not None:
+            line["rk4_companion"] = rk4
         print(json.dumps(line))
     if world > 1:
         dist.destroy_process_group()
