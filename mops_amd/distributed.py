@@ -17,6 +17,11 @@ from __future__ import annotations
 import numpy as np
 
 
+def _is_torch(a) -> bool:
+    # (numpy >= 2 arrays also have a `.device` attribute, so test the type)
+    return type(a).__module__.split(".")[0] == "torch"
+
+
 def shard_bounds(n_total: int, rank: int, world: int) -> tuple[int, int]:
     """Contiguous block [lo, hi) of particle indices owned by `rank`."""
     if world <= 0 or not (0 <= rank < world):
@@ -53,7 +58,7 @@ def unshard(gathered, n_total: int, world: int):
     for r in range(world):
         lo, hi = shard_bounds(n_total, r, world)
         parts.append(gathered[r][..., : hi - lo])
-    if hasattr(gathered, "device"):
+    if _is_torch(gathered):
         import torch
         return torch.cat(parts, dim=-1)
     return np.concatenate(parts, axis=-1)
@@ -66,7 +71,7 @@ def unshard_slots(gathered, gathered_ids, n_total: int, world: int):
     ``gathered_ids`` [world, n_pad]: rank r's ``ParticleSet.ids`` (slot -> local
     particle index within the rank's shard ``shard_bounds(n_total, r, world)``).
     """
-    is_torch = hasattr(gathered, "device")
+    is_torch = _is_torch(gathered)
     if is_torch:
         import torch
         out = torch.empty(tuple(gathered.shape[1:-1]) + (int(n_total),), dtype=gathered.dtype, device=gathered.device)

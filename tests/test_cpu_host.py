@@ -122,6 +122,36 @@ def test_shard_bounds_cover_exactly():
             assert max(h - l for l, h in spans) == max_shard(n, w) or n == 0
 
 
+def test_unshard_slots_inverts_any_slot_order():
+    """Property: whatever locality permutation each rank applied to its shard, gathering
+    the slot-ordered slabs (padded to the largest shard) with the ranks' slot ids and
+    unsharding gives the global particle order back; an id outside its shard is rejected."""
+    from hypothesis import given, settings, strategies as st
+    from mops_amd.distributed import max_shard, shard_bounds, unshard_slots
+
+    @settings(max_examples=60, deadline=None)
+    @given(n=st.integers(0, 300), world=st.integers(1, 9), seed=st.integers(0, 2**31 - 1))
+    def prop(n, world, seed):
+        rng = np.random.default_rng(seed)
+        truth = rng.standard_normal((2, n))
+        pad = max(1, max_shard(n, world))
+        slabs = np.full((world, 2, pad), np.nan)
+        ids = np.full((world, pad), -7, dtype=np.int32)
+        for r in range(world):
+            lo, hi = shard_bounds(n, r, world)
+            perm = rng.permutation(hi - lo).astype(np.int32)  # slot s holds local particle perm[s]
+            ids[r, : hi - lo] = perm
+            slabs[r, :, : hi - lo] = truth[:, lo + perm]
+        assert np.array_equal(unshard_slots(slabs, ids, n, world), truth)
+        if n > 0:
+            r = next(r for r in range(world) if shard_bounds(n, r, world)[1] > shard_bounds(n, r, world)[0])
+            bad = ids.copy()
+            bad[r, 0] = shard_bounds(n, r, world)[1] - shard_bounds(n, r, world)[0]
+            with pytest.raises(ValueError):
+                unshard_slots(slabs, bad, n, world)
+    prop()
+
+
 def test_record_period_rules():
     import math
     from mops_amd.engine import TrajectoryConfig
