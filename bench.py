@@ -630,9 +630,11 @@ def main_chain(args, mesh, dev, world, rank):
                     "daily pairs, snapshots generated + derived in HBM inside the timed region")
     else:
         workload = (f"oRRS18to6-class chained pathline (BASELINE config 5), {n:.3g} Gaussian Gulf-of-Mexico particles"
-                    f"/GPU, depth {args.depth:g} m, dt {args.dt} s, {args.pairs} monthly pair(s) of the 12 in the "
-                    "365-day run (a bounded sample; every pair is the same work shape), snapshots generated + "
-                    "derived in HBM inside the timed region")
+                    f"/GPU, depth {args.depth:g} m, dt {args.dt} s, "
+                    + (f"all {args.pairs} monthly pairs of the year-long run" if args.pairs >= 12 else
+                       f"{args.pairs} monthly pair(s) of the 12 in the year-long run (a bounded sample; every pair "
+                       "is the same work shape)")
+                    + ", snapshots generated + derived in HBM inside the timed region")
     if rank == 0:
         print(json.dumps({
             "metric": "particle-steps/sec", "value": value, "unit": "particle-steps/s", "n_gpus": world,
