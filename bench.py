@@ -325,12 +325,15 @@ def main():
 
     kernel_ms = []
     dispatch_ms = []  # per traj_kernel launch (HIP events on its part stream): what rocprofv3 averages
+    ev_ids, ev_ckpt = [None], [None]  # comm-stream events of the last slot-id / checkpoint gathers
 
     def one_call(timed: bool, pset=None):
         """One StreamLine call on this rank's shard (device resident); ``pset``: another ParticleSet
         of the same seeds (the RK4 companion line)."""
         ps_ = pset if pset is not None else ps
         with torch.cuda.stream(compute):
+            if ev_ids[0] is not None:  # the previous call's slot-id gather has read ids (reorder rewrites them)
+                compute.wait_event(ev_ids[0])
             ps_.reset(depth=args.depth)
             dmesh.locate(ps_.seeds.data_ptr(), ps_.cell.data_ptr(), n, stream=compute)  # seeds in slot order
             ps_.reorder(stream=compute)
@@ -340,6 +343,8 @@ def main():
                 comm.wait_event(sorted_ev)
                 with torch.cuda.stream(comm):
                     all_gather_flat(dist, gathered_ids.view(-1), ps_.ids, args.backend)
+                    ev_ids[0] = torch.cuda.Event()
+                    ev_ids[0].record(comm)
             for (s0, s1) in segments:
                 # the segment's trajectory launches: particle parts on their own streams, each in
                 # step chunks, so one part's final partial round of waves overlaps the others' work
@@ -367,6 +372,8 @@ def main():
                             for k in range(k0, k1):
                                 all_gather_flat(dist, gathered[k].view(-1), ps_.records[k].view(-1), args.backend)
             if world > 1:  # the checkpoint: every particle's final state on every rank
+                if ev_ckpt[0] is not None:  # the previous call's checkpoint gather has read ckpt
+                    compute.wait_event(ev_ckpt[0])
                 ckpt[0].copy_(ps_.x); ckpt[1].copy_(ps_.y); ckpt[2].copy_(ps_.z)
                 ckpt[3].copy_(ps_.depth); ckpt[4].copy_(ps_.death)
                 done = torch.cuda.Event()
@@ -374,8 +381,13 @@ def main():
                 comm.wait_event(done)
                 with torch.cuda.stream(comm):
                     all_gather_flat(dist, gathered_ckpt.view(-1), ckpt.view(-1), args.backend)
+                    ev_ckpt[0] = torch.cuda.Event()
+                    ev_ckpt[0].record(comm)
         compute.synchronize()
-        comm.synchronize()
+        if gather_records:  # the next call's reset rewrites the records these gathers read
+            comm.synchronize()
+        # checkpoint mode: this call's checkpoint gather overlaps the next call's compute (the events
+        # above order the buffers); the timed region's closing device synchronize waits for the last one
 
     for _ in range(args.warmup):
         one_call(False)
