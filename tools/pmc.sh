@@ -5,6 +5,8 @@
 set -u
 out=$1; shift
 export TMPDIR=/tmp
+# the counter passes must see only the measured workload's kernels (bench.py's RK4 companion off)
+export MOPS_BENCH_NO_RK4=1
 i=0
 mkdir -p "$out"
 for grp in "$@"; do

@@ -7,6 +7,8 @@ set -u
 out=${1:-gpurun_out/pmcc}
 mkdir -p "$out"
 export TMPDIR=/tmp
+# the counter passes must see only the measured workload's kernels (bench.py's RK4 companion off)
+export MOPS_BENCH_NO_RK4=1
 for c in "4:--pairs 2:orrs18to6_chain4_euler_10000000_seg720" "5:--pairs 1:orrs18to6_chain5_euler_12500000_seg4320"; do
   n=${c%%:*}; r=${c#*:}; a=${r%%:*}; key=${r#*:}
   timeout -k 5 400 rocprofv3 --pmc FETCH_SIZE --kernel-include-regex traj_kernel --output-format csv -d "$out/c$n/fetch" -o p -- \

@@ -5,6 +5,8 @@ set -u
 out=${1:-gpurun_out/c3}
 mkdir -p "$out"
 export TMPDIR=/tmp
+# the counter passes must see only the measured workload's kernels (bench.py's RK4 companion off)
+export MOPS_BENCH_NO_RK4=1
 timeout -k 10 400 python3 bench.py --config 3 --steps 1 --warmup 1 > "$out/bench.json" 2> "$out/bench.err" || { echo "bench failed"; exit 1; }
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$out/stats" -o p -- \
     python3 bench.py --config 3 --steps 1 --warmup 0 --no-cpu-baseline > "$out/stats.log" 2>&1 || { echo "stats failed"; exit 1; }

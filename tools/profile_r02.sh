@@ -8,6 +8,8 @@ set -u
 out=$1; key=$2; units=$3; shift 3
 mkdir -p "$out" "$out/pmc"
 export TMPDIR=/tmp
+# the counter passes must see only the measured workload's kernels (bench.py's RK4 companion off)
+export MOPS_BENCH_NO_RK4=1
 timeout -k 10 240 rocprofv3 --kernel-trace --stats --output-format csv -d "$out/stats" -o p -- \
     python3 bench.py --no-cpu-baseline "$@" > "$out/stats.log" 2>&1 || { echo "stats failed"; exit 1; }
 timeout -k 5 240 rocprofv3 --pmc FETCH_SIZE --kernel-include-regex traj_kernel --output-format csv -d "$out/fetch" -o p -- \
