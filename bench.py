@@ -5,9 +5,11 @@ Workload (BASELINE.json configs[1]): EC30to60-class mesh (synthetic, ~236k
 ocean cells, 60 levels), 1e6 particles per GPU, fixed depth 800 m,
 dt = 120 s, 1-day streamline (720 steps, Euler = the reference default),
 records every 3600 s.  One bench "step" = one complete StreamLine call on
-the rank's particle shard: seed location, 720 integration steps in 24
-record segments and -- for N > 1 -- an RCCL all-gather of each record slab
-over xGMI on a side stream, overlapped with the next segment's kernel.
+the rank's particle shard: seed location, locality order, the 720 integration
+steps (2 particle parts x 6 step chunks on two streams), the line assembly +
+NaN cleanup (the reference's FinalizeTrajectoryLines) and -- for N > 1 -- an
+RCCL all-gather of the final-state checkpoint over xGMI on a side stream.
+``--gpus N`` without a launcher starts the N ranks itself (torch.distributed.run).
 
 ``--config 3``: BASELINE configs[2] -- 1e7 particles/GPU, layer 10, dt 60 s,
 7-day pathline as 7 chained daily snapshot pairs (mops_amd/chain.py).
@@ -88,6 +90,9 @@ def parse():
                    help="configs 4/5: CUs reserved for a side stream that generates and derives snapshot p+2 while "
                         "pair p computes on the others (three field buffers); 0 = off (two buffers, derivation "
                         "between pairs, the default: measured slower, DESIGN.md section 3.3)")
+    p.add_argument("--compact", choices=["auto", "on", "off"], default="auto",
+                   help="config 2: re-sort each particle part with its dead particles last between step chunks "
+                        "(ParticleSet.compact); auto = on for RK4 (quirk Q1 kills half the particles in a day)")
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--cpu-seconds", type=float, default=12.0, help="target CPU-baseline sample length")
     return p.parse_args()
@@ -128,14 +133,11 @@ def make_gaussian_seeds(n: int, rank: int) -> np.ndarray:
 
 
 def engine_build_id() -> str:
-    """Identity of the trajectory kernel build: sha256 of the engine source and its hipcc flags
-    (tools/make_traffic.py stamps every PMC entry with it, so a changed kernel never inherits
-    another build's measured traffic)."""
-    import hashlib
-    import __graft_entry__ as g
-    h = hashlib.sha256(open(g.HIP_SRC, "rb").read())
-    h.update(" ".join(g.HIPCC_FLAGS[:-1]).encode())  # the -I path differs between machines
-    return h.hexdigest()[:16]
+    """Identity of the engine build (mops_amd/_build_id.py: sources, headers, hipcc flags, ROCm
+    release -- the id stamped into libmops_traj.so); tools/make_traffic.py stamps every PMC entry
+    with it, so a changed kernel never inherits another build's measured traffic."""
+    from mops_amd import _build_id
+    return _build_id.build_id()
 
 
 PEAK_FP64_TFLOPS = 78.6  # MI355X FP64 vector (spec; half of the guide's 157.3 TF FP32 vector rate)
@@ -250,8 +252,35 @@ def layer_mid_depth(mesh, layer: int = 10) -> float:
     return 0.5 * (float(mesh.refBottomDepth[layer - 1]) + float(mesh.refBottomDepth[layer]))
 
 
+def free_port() -> int:
+    import socket
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def launcher_command(gpus: int, argv, port: int) -> list:
+    """The one-process-per-GPU launch of this script for ``--gpus N`` (N > 1) when no launcher set
+    WORLD_SIZE: torch.distributed.run with N local ranks over 127.0.0.1, the same arguments."""
+    return [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={gpus}",
+            "--master-addr", "127.0.0.1", "--master-port", str(port), os.path.abspath(__file__), *argv]
+
+
+def check_world(gpus: int, world: int) -> None:
+    if world != gpus:
+        raise SystemExit(f"bench.py: --gpus {gpus} but the launcher started {world} rank(s) (WORLD_SIZE); "
+                         "run `python bench.py --gpus N` alone (it starts the ranks itself) or under "
+                         "torch.distributed.run with --nproc-per-node N")
+
+
 def main():
     args = parse()
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        # no launcher: start the N ranks as child processes (before anything touches the GPU; never
+        # exec) and exit with their status -- rank 0 prints the line
+        import subprocess
+        sys.exit(subprocess.run(launcher_command(args.gpus, sys.argv[1:], free_port())).returncode)
+    check_world(args.gpus, int(os.environ.get("WORLD_SIZE", "1")))
     if args.config in (3, 4, 5):  # config values for every option left at its config-2 default
         d = vars(argparse.Namespace(mode="streamline", particles=1_000_000, dt=120, duration=86400, record=3600,
                                     method="euler", depth=800.0, freq=158, levels=60))
@@ -324,6 +353,9 @@ def main():
             gathered = torch.empty((ps.K, world, 6, n), dtype=torch.float64, device=dev)
 
     kernel_ms = []
+    finalize_ms = []  # line assembly + NaN cleanup per call
+    lines_out = [None]  # the last call's finalized lines (kept alive until the next call)
+    compact = args.compact == "on" or (args.compact == "auto" and args.method == "rk4")
     dispatch_ms = []  # per traj_kernel launch (HIP events on its part stream): what rocprofv3 averages
     ev_ids, ev_ckpt = [None], [None]  # comm-stream events of the last slot-id / checkpoint gathers
 
@@ -356,7 +388,8 @@ def main():
                 # segments whose record gathers overlap the next one: short launches cost ~6% each)
                 nch = max(1, round(args.chunks * (s1 - s0) / n_steps))
                 ps_.advance_pipelined(dfield, dback, s0, s1, part_streams, nch,
-                                     timing=dispatch_ms if timed else None)
+                                     timing=dispatch_ms if timed else None,
+                                     compact=compact or (pset is not None and args.compact != "off"))
                 for st in part_streams:
                     j = torch.cuda.Event(); j.record(st); compute.wait_event(j)
                 e1.record(compute)
@@ -371,6 +404,14 @@ def main():
                         with torch.cuda.stream(comm):
                             for k in range(k0, k1):
                                 all_gather_flat(dist, gathered[k].view(-1), ps_.records[k].view(-1), args.backend)
+            # the reference's StreamLine ends by assembling the lines (FinalizeTrajectoryLines +
+            # RemoveNaN, MPASOVisualizerKernels.cpp:1005-1014): part of every call
+            f0 = torch.cuda.Event(enable_timing=True); f1 = torch.cuda.Event(enable_timing=True)
+            f0.record(compute)
+            lines_out[0] = ps_.finalize(pathline, stream=compute)
+            f1.record(compute)
+            if timed:
+                finalize_ms.append((f0, f1))
             if world > 1:  # the checkpoint: every particle's final state on every rank
                 if ev_ckpt[0] is not None:  # the previous call's checkpoint gather has read ckpt
                     compute.wait_event(ev_ckpt[0])
@@ -425,6 +466,7 @@ def main():
         att4 = torch.where(d4 < 0, torch.full_like(d4, n_steps), d4 + 1).sum().item()
         rk4 = {"value": att4 / el4, "unit": "particle-steps/s", "ms_per_call": el4 * 1e3,
                "dead_fraction": float((d4 >= 0).sum().item()) / max(n, 1),
+               "dead_particle_compaction": args.compact != "off",
                "note": "same workload integrated with RK4 (four evaluations per step in the step's start "
                        "cell, quirk Q1), one timed call after the Euler line; not part of value"}
         del ps4
@@ -452,6 +494,8 @@ def main():
                               f"{args.parts * args.chunks} overlapping traj_kernel launches)")
     roof["dispatches_per_unit"] = len(dms) / max(1, args.steps * len(segments))
     roof["avg_dispatch_ms"] = (sum(dms) / len(dms)) if dms else None  # = rocprofv3's traj_kernel average
+    fms = [a.elapsed_time(b) for (a, b) in finalize_ms]
+    finalize_avg = (sum(fms) / len(fms)) if fms else None
 
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
@@ -495,6 +539,11 @@ def main():
             "nominal_particle_steps_per_call": n_all * n_steps,
             "attempted_particle_steps_per_call": attempted_all,
             "dead_fraction": dead_all / max(n_all, 1),
+            "finalize": {"ms_per_call": finalize_avg,
+                         "share_of_step": (finalize_avg / (elapsed / args.steps * 1e3)) if finalize_avg else None,
+                         "what": "line assembly + NaN cleanup on device (assemble_kernel + remove_nan_kernel), "
+                                 "inside every timed call as in the reference's StreamLine"},
+            "dead_particle_compaction": compact,
             "roofline": roof,
             "cpu_baseline": cpu,
         }

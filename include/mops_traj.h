@@ -180,6 +180,19 @@ mops_status mops_locate_cells_hinted(const mops_mesh* mesh, int64_t n, const dou
 mops_status mops_order_particles(const mops_mesh* mesh, int64_t n, const int32_t* d_cell, int32_t* d_order,
                                  void* stream);
 
+/* Dead-particle compaction (no reference counterpart: the reference's
+ * parallel_for keeps visiting particles whose lambda has returned,
+ * MPASOVisualizerKernels.cpp:944-957, quirk Q1).  As mops_order_particles,
+ * but particles with d_death[i] >= 0 (d_death may be NULL) sort after every
+ * live one, so live particles fill whole waves and all-dead waves exit at
+ * their first instruction.  Re-entrant: the caller passes device scratch of
+ * at least mops_order_scratch_bytes(n) bytes, so several particle parts can
+ * be re-sorted concurrently on their own streams. */
+int64_t mops_order_scratch_bytes(int64_t n);
+mops_status mops_order_particles_live(const mops_mesh* mesh, int64_t n, const int32_t* d_cell,
+                                      const int32_t* d_death, int32_t* d_order, void* d_scratch,
+                                      int64_t scratch_bytes, void* stream);
+
 /* ---- trajectory hot path (device-resident) ----------------------------- */
 
 /* Number of record slots K = simulation_duration / record_t (reference
@@ -218,6 +231,22 @@ mops_status mops_traj_finalize(int64_t n, int64_t K, const double* d_seeds, cons
  * place (device pointers; [n*P*3], [n*P*3], [n*P], [n*P], out [n*3]). */
 mops_status mops_remove_nan_lines(int64_t n, int64_t P, double* d_points, double* d_velocity,
                                   double* d_temperature, double* d_salinity, double* d_last_point, void* stream);
+/* The same for ragged lines -- the reference's vector<TrajectoryLine>, whose
+ * lines may differ in length (RemoveNaNTrajectoriesAndReindex,
+ * src/Common/TrajectoryCommon.h:57-129; test/test_trajector.cpp:26-194):
+ * line i is points [d_offsets[i], d_offsets[i+1]) of the packed arrays
+ * (d_offsets [n+1], device), velocity/temperature/salinity already resized to
+ * the points' length (:88-90).  One launch for all lines; an empty line is
+ * left untouched (the reference drops it and re-indexes the rest, which is
+ * host bookkeeping).  d_last_point [n*3] gets each non-empty line's last point. */
+mops_status mops_remove_nan_ragged(int64_t n, const int64_t* d_offsets, double* d_points, double* d_velocity,
+                                   double* d_temperature, double* d_salinity, double* d_last_point, void* stream);
+
+/* Identity of the engine build: a hash of the engine's sources, headers,
+ * compiler flags and ROCm version, stamped at compile time (no reference
+ * counterpart).  The Python loader refuses a library whose id differs from
+ * the sources next to it, so a stale binary never runs. */
+const char* mops_build_id(void);
 
 /* ---- host convenience (the backend plug point) ------------------------- */
 

@@ -18,9 +18,10 @@ EXPORTED = (
     "mops_mesh_create", "mops_mesh_destroy", "mops_mesh_bytes",
     "mops_field_create", "mops_field_create_device", "mops_field_rebuild_device", "mops_field_create_derived", "mops_field_export", "mops_cell_to_vertex_attr",
     "mops_field_destroy", "mops_field_bytes",
-    "mops_locate_cells", "mops_locate_cells_hinted", "mops_order_particles",
+    "mops_locate_cells", "mops_locate_cells_hinted", "mops_order_particles", "mops_order_scratch_bytes",
+    "mops_order_particles_live",
     "mops_traj_num_records", "mops_traj_num_steps", "mops_traj_advance", "mops_traj_finalize",
-    "mops_remove_nan_lines", "mops_run_trajectories",
+    "mops_remove_nan_lines", "mops_remove_nan_ragged", "mops_run_trajectories", "mops_build_id",
     # include/mops_io.h
     "mops_lines_geo", "mops_write_lines_vtp", "mops_write_lines_txt", "mops_write_pathline_binary",
     # include/mops_netcdf.h
@@ -86,6 +87,17 @@ def load(path: str | None = None):
     st = C.c_int
     lib.mops_last_error.restype = C.c_char_p
     lib.mops_abi_version.restype = I32
+    if os.path.abspath(path) == os.path.abspath(LIB_PATH):
+        # the product library must be the build of the sources next to it (experiment variants
+        # loaded through MOPS_TRAJ_LIB are exempt)
+        from . import _build_id
+        lib.mops_build_id.restype = C.c_char_p
+        have = lib.mops_build_id().decode(errors="replace")
+        want = _build_id.MARKER + _build_id.build_id()
+        if have != want:
+            raise MopsError(f"stale engine library {path}: built as {have!r}, the sources are {want!r}; rebuild with "
+                            "`python -c \"import __graft_entry__ as g; g.build()\"`")
+    lib.mops_build_id.restype = C.c_char_p
     if hasattr(lib, "mops_selftest_math"):  # (older engine builds timed as variants lack the self-test)
         lib.mops_selftest_math.argtypes = [I64, P, P, I32, P]; lib.mops_selftest_math.restype = st
     lib.mops_mesh_create.argtypes = [P, P, P]; lib.mops_mesh_create.restype = st
@@ -121,6 +133,10 @@ def load(path: str | None = None):
     lib.mops_traj_finalize.argtypes = [I64, I64, P, P, I64, I32, P, P, P, P, P, P, P]
     lib.mops_traj_finalize.restype = st
     lib.mops_remove_nan_lines.argtypes = [I64, I64, P, P, P, P, P, P]; lib.mops_remove_nan_lines.restype = st
+    lib.mops_remove_nan_ragged.argtypes = [I64, P, P, P, P, P, P, P]; lib.mops_remove_nan_ragged.restype = st
+    lib.mops_order_scratch_bytes.argtypes = [I64]; lib.mops_order_scratch_bytes.restype = I64
+    lib.mops_order_particles_live.argtypes = [P, I64, P, P, P, P, I64, P]
+    lib.mops_order_particles_live.restype = st
     lib.mops_run_trajectories.argtypes = [P, P, P, P, I64, P, P, C.c_float, P, P, P, P, P, P, P, P, P, P]
     lib.mops_run_trajectories.restype = st
     _lib = lib

@@ -92,17 +92,23 @@ class PathlineChain:
             pdep = (torch.as_tensor(np.asarray(particle_depths, dtype=np.float32), device=dev) if per_particle
                     else None)
 
+        recycle = self.own_fields and not self.prefetch and hasattr(self.make_field, "refill")
+        overlap = recycle and self.overlap_stream is not None
+        if overlap and self.n_snapshots > 2 and not hasattr(self.make_field, "pool"):
+            raise ValueError("overlap_stream needs a recycling make_field with a buffer pool "
+                             "(synth_device.DeviceFieldRecycler)")
         fields = {}
         with torch.cuda.stream(cs):
             fields[0] = self.make_field(0, cs.cuda_stream)
             fields[1] = self.make_field(1, cs.cuda_stream)
+            if overlap and self.n_snapshots > 2 and len(self.make_field.pool) < 1:
+                raise ValueError("overlap_stream needs a third field buffer in make_field.pool (seed the "
+                                 "recycler with three fields and release them before the run)")
             ps = ParticleSet(self.mesh, seeds0, cfg.depth, cfg, device=dev)
         period = ps.record_period(pathline=True)
         pts_acc, vel_acc, tmp_acc, sal_acc = [], [], [], []
         last = None
         attempted = torch.zeros((), dtype=torch.int64, device=dev)
-        recycle = self.own_fields and not self.prefetch and hasattr(self.make_field, "refill")
-        overlap = recycle and self.overlap_stream is not None
         ov = self.overlap_stream
         ready, pair_done = {}, {}
         for p in range(self.n_snapshots - 1):

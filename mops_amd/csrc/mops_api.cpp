@@ -18,6 +18,7 @@
 #include <stdexcept>
 
 namespace MOPS {
+static_assert(sizeof(CartesianCoord) == 3 * sizeof(double), "CartesianCoord is packed xyz (host <-> device copies)");
 namespace {
 
 void Error(const char* fmt, ...) {
@@ -382,36 +383,71 @@ double MOPS_GetTotalTime() {
     return s;
 }
 
+// RemoveNaNTrajectoriesAndReindex (src/Common/TrajectoryCommon.h:57-129): every non-empty line
+// packed into one device allocation, cleaned by ONE mops_remove_nan_ragged launch, copied back.
 std::vector<TrajectoryLine> RemoveNaNTrajectoriesAndReindex(std::vector<TrajectoryLine>& lines) {
-    std::vector<TrajectoryLine> out;
-    out.reserve(lines.size());
-    int new_id = 0;
+    std::vector<TrajectoryLine*> keep;  // empty lines are dropped (:84-86)
+    keep.reserve(lines.size());
+    std::vector<int64_t> off(1, 0);
     for (auto& l : lines) {
         const size_t P = l.points.size();
-        if (P == 0) continue;  // TrajectoryCommon.h:84-86
-        l.velocity.resize(P, CartesianCoord{0.0, 0.0, 0.0});
+        if (P == 0) continue;
+        l.velocity.resize(P, CartesianCoord{0.0, 0.0, 0.0});  // :88-90
         l.temperature.resize(P, 0.0);
         l.salinity.resize(P, 0.0);
-        double *dp = nullptr, *dv = nullptr, *dt = nullptr, *ds = nullptr, *dl = nullptr;
-        check(hipMalloc(&dp, P * 24) == hipSuccess && hipMalloc(&dv, P * 24) == hipSuccess &&
-                      hipMalloc(&dt, P * 8) == hipSuccess && hipMalloc(&ds, P * 8) == hipSuccess &&
-                      hipMalloc(&dl, 24) == hipSuccess
-                  ? MOPS_OK
-                  : MOPS_ERR_HIP,
-              "hipMalloc");
-        (void)hipMemcpy(dp, l.points.data(), P * 24, hipMemcpyHostToDevice);
-        (void)hipMemcpy(dv, l.velocity.data(), P * 24, hipMemcpyHostToDevice);
-        (void)hipMemcpy(dt, l.temperature.data(), P * 8, hipMemcpyHostToDevice);
-        (void)hipMemcpy(ds, l.salinity.data(), P * 8, hipMemcpyHostToDevice);
-        const mops_status st = mops_remove_nan_lines(1, (int64_t)P, dp, dv, dt, ds, dl, nullptr);
-        (void)hipMemcpy(l.points.data(), dp, P * 24, hipMemcpyDeviceToHost);
-        (void)hipMemcpy(l.velocity.data(), dv, P * 24, hipMemcpyDeviceToHost);
-        (void)hipMemcpy(l.temperature.data(), dt, P * 8, hipMemcpyDeviceToHost);
-        (void)hipMemcpy(l.salinity.data(), ds, P * 8, hipMemcpyDeviceToHost);
-        (void)hipMemcpy(&l.lastPoint, dl, 24, hipMemcpyDeviceToHost);
-        (void)hipFree(dp); (void)hipFree(dv); (void)hipFree(dt); (void)hipFree(ds); (void)hipFree(dl);
-        check(st, "mops_remove_nan_lines");
-        l.lineID = new_id++;
+        keep.push_back(&l);
+        off.push_back(off.back() + (int64_t)P);
+    }
+    const int64_t m = (int64_t)keep.size(), T = off.back();
+    std::vector<TrajectoryLine> out;
+    out.reserve((size_t)m);
+    if (m == 0) return out;
+    std::vector<double> hp((size_t)T * 3), hv((size_t)T * 3), ht((size_t)T), hs((size_t)T), hl((size_t)m * 3);
+    for (int64_t i = 0; i < m; ++i) {
+        const TrajectoryLine& l = *keep[(size_t)i];
+        const size_t P = l.points.size(), b = (size_t)off[(size_t)i];
+        std::memcpy(hp.data() + 3 * b, l.points.data(), P * sizeof(CartesianCoord));
+        std::memcpy(hv.data() + 3 * b, l.velocity.data(), P * sizeof(CartesianCoord));
+        std::memcpy(ht.data() + b, l.temperature.data(), P * sizeof(double));
+        std::memcpy(hs.data() + b, l.salinity.data(), P * sizeof(double));
+    }
+    // one allocation: points | velocity | temperature | salinity | last | offsets
+    const size_t bytes = (size_t)T * 64 + (size_t)m * 24 + (size_t)(m + 1) * 8;
+    struct DevBuf {
+        void* p = nullptr;
+        ~DevBuf() { (void)hipFree(p); }
+    } buf;
+    auto hip = [](hipError_t e, const char* what) {
+        if (e != hipSuccess) throw std::runtime_error(std::string(what) + ": " + hipGetErrorString(e));
+    };
+    hip(hipMalloc(&buf.p, bytes), "RemoveNaNTrajectoriesAndReindex: hipMalloc");
+    double* dp = static_cast<double*>(buf.p);
+    double* dv = dp + 3 * T;
+    double* dt = dv + 3 * T;
+    double* ds = dt + T;
+    double* dl = ds + T;
+    int64_t* doff = reinterpret_cast<int64_t*>(dl + 3 * m);
+    const hipMemcpyKind h2d = hipMemcpyHostToDevice, d2h = hipMemcpyDeviceToHost;
+    hip(hipMemcpy(dp, hp.data(), (size_t)T * 24, h2d), "hipMemcpy points");
+    hip(hipMemcpy(dv, hv.data(), (size_t)T * 24, h2d), "hipMemcpy velocity");
+    hip(hipMemcpy(dt, ht.data(), (size_t)T * 8, h2d), "hipMemcpy temperature");
+    hip(hipMemcpy(ds, hs.data(), (size_t)T * 8, h2d), "hipMemcpy salinity");
+    hip(hipMemcpy(doff, off.data(), (size_t)(m + 1) * 8, h2d), "hipMemcpy offsets");
+    check(mops_remove_nan_ragged(m, doff, dp, dv, dt, ds, dl, nullptr), "mops_remove_nan_ragged");
+    hip(hipMemcpy(hp.data(), dp, (size_t)T * 24, d2h), "hipMemcpy points");
+    hip(hipMemcpy(hv.data(), dv, (size_t)T * 24, d2h), "hipMemcpy velocity");
+    hip(hipMemcpy(ht.data(), dt, (size_t)T * 8, d2h), "hipMemcpy temperature");
+    hip(hipMemcpy(hs.data(), ds, (size_t)T * 8, d2h), "hipMemcpy salinity");
+    hip(hipMemcpy(hl.data(), dl, (size_t)m * 24, d2h), "hipMemcpy lastPoint");
+    for (int64_t i = 0; i < m; ++i) {
+        TrajectoryLine& l = *keep[(size_t)i];
+        const size_t P = l.points.size(), b = (size_t)off[(size_t)i];
+        std::memcpy(l.points.data(), hp.data() + 3 * b, P * sizeof(CartesianCoord));
+        std::memcpy(l.velocity.data(), hv.data() + 3 * b, P * sizeof(CartesianCoord));
+        std::memcpy(l.temperature.data(), ht.data() + b, P * sizeof(double));
+        std::memcpy(l.salinity.data(), hs.data() + b, P * sizeof(double));
+        l.lastPoint = {hl[(size_t)(3 * i)], hl[(size_t)(3 * i + 1)], hl[(size_t)(3 * i + 2)]};  // :123
+        l.lineID = (int)i;  // :124
         out.push_back(l);
     }
     return out;

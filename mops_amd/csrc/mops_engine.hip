@@ -38,7 +38,10 @@
 #include "mops_io.h"
 #include "mops_traj.h"
 
-#define MOPS_ABI_VERSION 2
+#define MOPS_ABI_VERSION 3
+#ifndef MOPS_BUILD_ID
+#define MOPS_BUILD_ID "unstamped"  // __graft_entry__.build_engine passes the sources' identity (mops_build_id)
+#endif
 
 namespace {
 
@@ -1406,14 +1409,20 @@ __global__ void lines_geo_kernel(int64_t m, const double* __restrict__ pts, cons
 
 __device__ __forceinline__ bool finite3(double a, double b, double c) { return isfinite(a) && isfinite(b) && isfinite(c); }
 
-__global__ void remove_nan_kernel(int64_t n, int64_t P, double* pts, double* vel, double* tmp, double* sal,
-                                  double* last) {
+// One thread per line.  Uniform lines (off == NULL): line i is points [i*P, (i+1)*P); ragged
+// lines: [off[i], off[i+1]) -- the reference's per-line vectors packed back to back.  An empty
+// line is left alone (the reference drops it, TrajectoryCommon.h:84-86: the host re-indexes).
+__global__ void remove_nan_kernel(int64_t n, int64_t P, const int64_t* __restrict__ off, double* pts, double* vel,
+                                  double* tmp, double* sal, double* last) {
     const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n) return;
-    double* pp = pts + 3 * i * P;
-    double* vv = vel ? vel + 3 * i * P : nullptr;
-    double* tt = tmp ? tmp + i * P : nullptr;
-    double* ss = sal ? sal + i * P : nullptr;
+    const int64_t b = off ? off[i] : i * P;
+    if (off) P = off[i + 1] - b;
+    if (P <= 0) return;
+    double* pp = pts + 3 * b;
+    double* vv = vel ? vel + 3 * b : nullptr;
+    double* tt = tmp ? tmp + b : nullptr;
+    double* ss = sal ? sal + b : nullptr;
     int64_t k = 0;
     for (; k < P; ++k)
         if (!finite3(pp[3 * k], pp[3 * k + 1], pp[3 * k + 2])) break;
@@ -1966,12 +1975,15 @@ __global__ void cell_key_kernel(int64_t C, const double4* cxyz, uint64_t* key) {
     key[i] = (spread3(qx) << 2) | (spread3(qy) << 1) | spread3(qz);
 }
 
-__global__ void particle_key_kernel(int64_t n, int64_t C, const int* cell, const uint64_t* cell_key, uint64_t* key,
-                                    int* idx) {
+// Morton key of each particle's cell; a dead particle (death >= 0, when given) or one without a
+// cell sorts last (~0), so live particles fill whole waves and all-dead waves exit at once
+__global__ void particle_key_kernel(int64_t n, int64_t C, const int* cell, const int* death,
+                                    const uint64_t* cell_key, uint64_t* key, int* idx) {
     const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n) return;
     const int c = cell[i];
-    key[i] = (c >= 0 && c < C) ? cell_key[c] : ~0ULL;
+    const bool live = !death || death[i] < 0;
+    key[i] = (live && c >= 0 && c < C) ? cell_key[c] : ~0ULL;
     idx[i] = (int)i;
 }
 
@@ -2109,8 +2121,11 @@ mops_status mops_mesh_create(const mops_mesh_desc* desc, void* stream, mops_mesh
         return fail(MOPS_ERR_INVALID, "mops_mesh_create: invalid sizes");
     if (maxE > kMaxVertex)
         return fail(MOPS_ERR_UNSUPPORTED, "mops_mesh_create: maxEdges > 20 (reference MAX_VERTEX_NUM)");
-    if (V * (int64_t)L >= INT32_MAX)  // level-pair record indices are 32-bit (dev::pair_sums)
+    // level-pair record indices are 32-bit (dev::pair_sums): V*(L-1) + 1 records < 2^31
+    if (V * (int64_t)L >= INT32_MAX)
         return fail(MOPS_ERR_UNSUPPORTED, "mops_mesh_create: nVertices * nVertLevels >= 2^31");
+    if (C > ((int64_t)1 << 30))  // the bucket directory's 32-bit size doubles up to 2C slots
+        return fail(MOPS_ERR_UNSUPPORTED, "mops_mesh_create: nCells > 2^30");
     if (!desc->h_n_edges_on_cell || !desc->h_vertices_on_cell || !desc->h_cells_on_cell || !desc->h_cell_coord ||
         !desc->h_vertex_coord)
         return fail(MOPS_ERR_INVALID, "mops_mesh_create: missing mesh array");
@@ -2514,7 +2529,42 @@ mops_status mops_order_particles(const mops_mesh* mesh, int64_t n, const int32_t
     uint64_t* kout = (uint64_t*)(base + a8);
     int* vin = (int*)(base + 2 * a8);
     void* tmp = base + 2 * a8 + a4;
-    particle_key_kernel<<<grid_for(n), kBlock, 0, s>>>(n, mesh->C, d_cell, mesh->d_cell_key, kin, vin);
+    particle_key_kernel<<<grid_for(n), kBlock, 0, s>>>(n, mesh->C, d_cell, nullptr, mesh->d_cell_key, kin, vin);
+    HIP_TRY(hipGetLastError());
+    HIP_TRY(hipcub::DeviceRadixSort::SortPairs(tmp, tmp_bytes, kin, kout, vin, d_order, (int)n, 0, 64, s));
+    return MOPS_OK;
+}
+
+int64_t mops_order_scratch_bytes(int64_t n) {
+    if (n <= 0 || n >= INT32_MAX) return 0;
+    size_t tmp_bytes = 0;
+    if (hipcub::DeviceRadixSort::SortPairs(nullptr, tmp_bytes, (const uint64_t*)nullptr, (uint64_t*)nullptr,
+                                           (const int*)nullptr, (int*)nullptr, (int)n, 0, 64, (hipStream_t)0) !=
+        hipSuccess)
+        return 0;
+    const size_t a8 = ((size_t)n * 8 + 255) / 256 * 256, a4 = ((size_t)n * 4 + 255) / 256 * 256;
+    return (int64_t)(2 * a8 + a4 + tmp_bytes + 256);
+}
+
+mops_status mops_order_particles_live(const mops_mesh* mesh, int64_t n, const int32_t* d_cell, const int32_t* d_death,
+                                      int32_t* d_order, void* d_scratch, int64_t scratch_bytes, void* stream) {
+    if (!mesh || n < 0 || (n > 0 && (!d_cell || !d_order || !d_scratch)) || n >= INT32_MAX)
+        return fail(MOPS_ERR_INVALID, "mops_order_particles_live: invalid argument");
+    if (n == 0) return MOPS_OK;
+    const int64_t need = mops_order_scratch_bytes(n);
+    if (need <= 0 || scratch_bytes < need)
+        return fail(MOPS_ERR_INVALID, "mops_order_particles_live: scratch smaller than mops_order_scratch_bytes(n)");
+    hipStream_t s = (hipStream_t)stream;
+    size_t tmp_bytes = 0;
+    HIP_TRY(hipcub::DeviceRadixSort::SortPairs(nullptr, tmp_bytes, (const uint64_t*)nullptr, (uint64_t*)nullptr,
+                                               (const int*)nullptr, (int*)nullptr, (int)n, 0, 64, s));
+    const size_t a8 = ((size_t)n * 8 + 255) / 256 * 256, a4 = ((size_t)n * 4 + 255) / 256 * 256;
+    char* base = (char*)(((uintptr_t)d_scratch + 255) / 256 * 256);  // the 256-B slack in the size covers this
+    uint64_t* kin = (uint64_t*)base;
+    uint64_t* kout = (uint64_t*)(base + a8);
+    int* vin = (int*)(base + 2 * a8);
+    void* tmp = base + 2 * a8 + a4;
+    particle_key_kernel<<<grid_for(n), kBlock, 0, s>>>(n, mesh->C, d_cell, d_death, mesh->d_cell_key, kin, vin);
     HIP_TRY(hipGetLastError());
     HIP_TRY(hipcub::DeviceRadixSort::SortPairs(tmp, tmp_bytes, kin, kout, vin, d_order, (int)n, 0, 64, s));
     return MOPS_OK;
@@ -2595,7 +2645,7 @@ mops_status mops_traj_finalize(int64_t n, int64_t K, const double* d_seeds, cons
     assemble_kernel<<<(unsigned)((n + kAsmSlots - 1) / kAsmSlots), 256, 0, s>>>(n, K, d_seeds, d_records, stride,
                                                                                pathline, d_line, d_points, d_vel,
                                                                                d_tmp, d_sal);
-    remove_nan_kernel<<<grid_for(n), kBlock, 0, s>>>(n, K + 1, d_points, d_vel, d_tmp, d_sal, d_last);
+    remove_nan_kernel<<<grid_for(n), kBlock, 0, s>>>(n, K + 1, nullptr, d_points, d_vel, d_tmp, d_sal, d_last);
     HIP_TRY(hipGetLastError());
     return MOPS_OK;
 }
@@ -2620,10 +2670,24 @@ mops_status mops_remove_nan_lines(int64_t n, int64_t P, double* d_points, double
                                   double* d_last, void* stream) {
     if (n < 0 || P <= 0 || !d_points) return fail(MOPS_ERR_INVALID, "mops_remove_nan_lines: invalid argument");
     if (n == 0) return MOPS_OK;
-    remove_nan_kernel<<<grid_for(n), kBlock, 0, (hipStream_t)stream>>>(n, P, d_points, d_vel, d_tmp, d_sal, d_last);
+    remove_nan_kernel<<<grid_for(n), kBlock, 0, (hipStream_t)stream>>>(n, P, nullptr, d_points, d_vel, d_tmp, d_sal,
+                                                                        d_last);
     HIP_TRY(hipGetLastError());
     return MOPS_OK;
 }
+
+mops_status mops_remove_nan_ragged(int64_t n, const int64_t* d_offsets, double* d_points, double* d_vel,
+                                   double* d_tmp, double* d_sal, double* d_last, void* stream) {
+    if (n < 0 || (n > 0 && (!d_offsets || !d_points)))
+        return fail(MOPS_ERR_INVALID, "mops_remove_nan_ragged: invalid argument");
+    if (n == 0) return MOPS_OK;
+    remove_nan_kernel<<<grid_for(n), kBlock, 0, (hipStream_t)stream>>>(n, 0, d_offsets, d_points, d_vel, d_tmp, d_sal,
+                                                                        d_last);
+    HIP_TRY(hipGetLastError());
+    return MOPS_OK;
+}
+
+const char* mops_build_id(void) { return MOPS_BUILD_ID; }
 
 mops_status mops_run_trajectories(const mops_mesh* mesh, const mops_field* front, const mops_field* back,
                                   const mops_traj_cfg* cfg, int64_t n, const double* h_seeds, const float* h_depths,

@@ -84,6 +84,11 @@ def unshard_slots(gathered, gathered_ids, n_total: int, world: int):
         ids = ids.long() if is_torch else np.asarray(ids, dtype=np.int64)
         if hi > lo and (int(ids.min()) < 0 or int(ids.max()) >= hi - lo):
             raise ValueError(f"rank {r}: slot ids outside its shard")
+        # a permutation of the shard: each local id exactly once (a duplicate would leave another
+        # particle's column unwritten)
+        counts = (torch.bincount(ids, minlength=hi - lo) if is_torch else np.bincount(ids, minlength=hi - lo))
+        if hi > lo and not bool((counts == 1).all()):
+            raise ValueError(f"rank {r}: slot ids are not a permutation of its shard")
         out[..., lo + ids] = gathered[r][..., : hi - lo]
         seen += hi - lo
     if seen != n_total:

@@ -269,6 +269,7 @@ class ParticleSet:
         # locality order (state loads/stores and record stores coalesce);
         # finalize() writes line ids[slot], so outputs keep the seed order
         self.ids = torch.arange(self.n, dtype=torch.int32, device=dev)
+        self._compact_scratch = {}
         self._written = False
         self._c = cfg.ctype()
         self.reorder(stream=torch.cuda.current_stream(dev).cuda_stream)
@@ -300,9 +301,45 @@ class ParticleSet:
         out[self.ids.long()] = t
         return out
 
-    def reset(self, seeds_xyz=None, depth=None):
-        if seeds_xyz is not None:
-            raise NotImplementedError
+    def compact(self, lo: int, hi: int, stream, records_written: int):
+        """Dead-particle compaction of slots [lo, hi) on ``stream`` (mops_order_particles_live):
+        live particles in the Morton order of their current cell first, dead ones after them, so
+        the next launches run full waves of live lanes and all-dead waves exit at once.  The SoA
+        state, seeds, slot ids and the first ``records_written`` record slots are permuted with
+        them (later slots are still all zero); results are unchanged (every particle is
+        independent, finalize writes each slot's line at its id).  Re-entrant across disjoint
+        ranges on different streams (each range has its own scratch)."""
+        torch = self.torch
+        n = hi - lo
+        if n <= 1:
+            return
+        lib = L.load()
+        s = stream if isinstance(stream, torch.cuda.Stream) else torch.cuda.ExternalStream(int(stream))
+        key = (lo, hi)
+        if key not in self._compact_scratch:
+            nb = int(lib.mops_order_scratch_bytes(n))
+            if nb <= 0:
+                raise L.MopsError("mops_order_scratch_bytes failed")
+            with torch.cuda.stream(s):
+                self._compact_scratch[key] = torch.empty((nb,), dtype=torch.uint8, device=self.seeds.device)
+        scratch = self._compact_scratch[key]
+        e4 = 4
+        L.check(lib.mops_order_particles_live(self.mesh.handle, n, C.c_void_p(self.cell.data_ptr() + e4 * lo),
+                                              C.c_void_p(self.death.data_ptr() + e4 * lo),
+                                              C.c_void_p(self.order.data_ptr() + e4 * lo),
+                                              C.c_void_p(scratch.data_ptr()), scratch.numel(), _stream_handle(s)),
+                "mops_order_particles_live")
+        with torch.cuda.stream(s):
+            o = self.order[lo:hi].long()
+            for t in (self.x, self.y, self.z, self.depth, self.cell, self.death, self.ids):
+                t[lo:hi].copy_(t[lo:hi][o])
+            self.seeds[lo:hi].copy_(self.seeds[lo:hi][o])
+            k = min(int(records_written), self.records.shape[0])
+            if k > 0:
+                r = self.records[:k, :, lo:hi]
+                r.copy_(r[:, :, o])
+
+    def reset(self, depth=None):
         self.x.copy_(self.seeds[:, 0]); self.y.copy_(self.seeds[:, 1]); self.z.copy_(self.seeds[:, 2])
         if depth is not None:
             self.depth.fill_(float(depth))
@@ -356,7 +393,7 @@ class ParticleSet:
                            self.cell.data_ptr() + e4 * lo, self.death.data_ptr() + e4 * lo, None)
 
     def advance_pipelined(self, front: DeviceField, back: DeviceField | None, step_begin: int, step_end: int,
-                          streams, chunks: int, timing=None):
+                          streams, chunks: int, timing=None, compact: bool = False):
         """``advance`` split into len(streams) contiguous particle parts (whole waves), each on its own
         stream, and ``chunks`` step ranges per part, enqueued chunk-major.
 
@@ -366,7 +403,11 @@ class ParticleSet:
         other parts' next chunk (kernel boundaries order each part's chunks; results are
         identical for any split: every particle is independent and records are indexed by
         absolute step).  The streams must already be ordered after the state's producers; the
-        caller joins them afterwards.  ``timing`` receives (start, end) events per launch."""
+        caller joins them afterwards.  ``timing`` receives (start, end) events per launch.
+        ``compact``: before every chunk but the first, each part is re-sorted on its own stream
+        with its dead particles last (``compact``): RK4 kills particles at cell crossings
+        (quirk Q1, half of them in a day at config 2), and a wave keeps its slots until its
+        last live lane finishes."""
         torch = self.torch
         nparts = max(1, len(streams))
         waves = -(-self.n // 64)
@@ -374,6 +415,7 @@ class ParticleSet:
         span = int(step_end) - int(step_begin)
         chunks = max(1, min(int(chunks), span))
         tb = [int(step_begin) + span * k // chunks for k in range(chunks + 1)]
+        period = self.record_period(pathline=back is not None)
         lib = L.load()
         for t in range(chunks):
             for k in range(nparts):
@@ -381,6 +423,9 @@ class ParticleSet:
                 if hi <= lo or tb[t + 1] <= tb[t]:
                     continue
                 st = streams[k]
+                if compact and t > 0:
+                    # slots written so far: slot 0 (step-0 pre-writes) .. the last completed record
+                    self.compact(lo, hi, st, records_written=min(self.K, tb[t] // period + 1) if period else 1)
                 if timing is not None:
                     e0 = torch.cuda.Event(enable_timing=True); e1 = torch.cuda.Event(enable_timing=True)
                     e0.record(st)

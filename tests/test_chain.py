@@ -6,8 +6,13 @@ import pytest
 EARTH_RADIUS_M = 6_371_000.0
 
 
-def oracle_chain(O, mesh, snaps, seeds, depth, particle_depths, gap, dt, rT, euler, follow_last=True):
-    derived = [O.preprocess(mesh, s) for s in snaps]
+def oracle_chain(O, mesh, snaps, seeds, depth, particle_depths, gap, dt, rT, euler, follow_last=True,
+                 derived=None):
+    """MOPSPathline.run semantics on the oracle; ``derived`` (oracle.Derived per snapshot) replaces
+    the host preprocessing of ``snaps`` (e.g. fields exported from HBM at oRRS18to6 size)."""
+    if derived is None:
+        derived = [O.preprocess(mesh, s) for s in snaps]
+    snaps = derived
     pts, vel, tmp, sal = [], [], [], []
     last = None
     pdep = None if particle_depths is None else np.asarray(particle_depths, dtype=np.float32)

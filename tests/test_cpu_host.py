@@ -2,6 +2,7 @@
 compute), host logic, and the multi-rank sharding with gloo."""
 import os
 import re
+import sys
 
 import numpy as np
 import pytest
@@ -72,7 +73,7 @@ def test_abi_exports_every_header_symbol(engine_lib):
 def test_abi_host_only_calls(engine_lib):
     import ctypes as C
     from mops_amd import _lib
-    assert engine_lib.mops_abi_version() == 2
+    assert engine_lib.mops_abi_version() == 3
     cfg = _lib.TrajCfg(120, 86400, 3600, 0, 1)
     assert engine_lib.mops_traj_num_records(C.byref(cfg)) == 24
     assert engine_lib.mops_traj_num_steps(C.byref(cfg)) == 720
@@ -149,6 +150,11 @@ def test_unshard_slots_inverts_any_slot_order():
             bad[r, 0] = shard_bounds(n, r, world)[1] - shard_bounds(n, r, world)[0]
             with pytest.raises(ValueError):
                 unshard_slots(slabs, bad, n, world)
+            if shard_bounds(n, r, world)[1] - shard_bounds(n, r, world)[0] >= 2:
+                dup = ids.copy()
+                dup[r, 1] = dup[r, 0]  # a duplicated id would leave another particle's column unwritten
+                with pytest.raises(ValueError):
+                    unshard_slots(slabs, dup, n, world)
     prop()
 
 
@@ -265,3 +271,86 @@ def test_sharded_records_gloo_world2():
         p.join(timeout=240)
     assert all(p.exitcode == 0 for p in procs)
     assert q.get(timeout=5) is True
+
+
+# ---------------------------------------------------------------- bench launcher / build identity
+def _bench():
+    import importlib.util
+    spec = importlib.util.spec_from_file_location("bench_under_test", os.path.join(ROOT, "bench.py"))
+    b = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(b)
+    return b
+
+
+def test_bench_gpus_n_starts_its_own_ranks(monkeypatch):
+    """`python bench.py --gpus N` (N > 1) with no launcher starts N ranks itself -- torch.distributed.run
+    over 127.0.0.1 with the same arguments, as a child process (never exec) -- and exits with its status;
+    under a launcher, a world size that differs from --gpus fails loudly."""
+    import subprocess
+    b = _bench()
+    seen = {}
+
+    class Done:
+        returncode = 3
+
+    def fake_run(cmd, *a, **k):
+        seen["cmd"] = cmd
+        return Done()
+
+    monkeypatch.delenv("WORLD_SIZE", raising=False)
+    monkeypatch.setattr(subprocess, "run", fake_run)
+    monkeypatch.setattr(sys, "argv", ["bench.py", "--gpus", "4", "--steps", "2", "--backend", "gloo"])
+    with pytest.raises(SystemExit) as e:
+        b.main()
+    assert e.value.code == 3
+    cmd = seen["cmd"]
+    assert cmd[1:3] == ["-m", "torch.distributed.run"] and "--nproc-per-node=4" in cmd
+    assert cmd[cmd.index("--master-addr") + 1] == "127.0.0.1"
+    assert cmd[-6:] == ["--gpus", "4", "--steps", "2", "--backend", "gloo"]
+    assert os.path.samefile(cmd[-7], os.path.join(ROOT, "bench.py"))
+    # launched by torchrun: WORLD_SIZE must equal --gpus
+    monkeypatch.setenv("WORLD_SIZE", "2")
+    monkeypatch.setattr(sys, "argv", ["bench.py", "--gpus", "4"])
+    with pytest.raises(SystemExit) as e:
+        b.main()
+    assert "--gpus 4" in str(e.value.code)
+    b.check_world(2, 2)  # consistent: no error
+
+
+def test_build_id_is_stamped_and_checked(engine_lib, tmp_path):
+    """libmops_traj.so carries the build id of the sources next to it (mops_build_id), the loader
+    refuses a library stamped with another id, and the id tracks every engine source and header."""
+    import shutil
+    from mops_amd import _build_id, _lib
+    bid = _build_id.build_id()
+    assert engine_lib.mops_build_id() == (_build_id.MARKER + bid).encode()
+    assert _build_id.stamped_id(_lib.LIB_PATH) == bid
+    assert len(_build_id.SOURCES) == 4 and all(os.path.exists(p) for p in _build_id.SOURCES + _build_id.HEADERS)
+    # a stale library (other stamp) at the product path is refused
+    stale = tmp_path / "libmops_traj.so"
+    data = open(_lib.LIB_PATH, "rb").read().replace(bid.encode(), b"0" * 16)
+    stale.write_bytes(data)
+    saved_lib, saved_path = _lib._lib, _lib.LIB_PATH
+    try:
+        _lib._lib = None
+        _lib.LIB_PATH = str(stale)
+        with pytest.raises(_lib.MopsError, match="stale engine library"):
+            _lib.load(str(stale))
+    finally:
+        _lib._lib, _lib.LIB_PATH = saved_lib, saved_path
+    assert shutil.which("hipcc") is None or bid != _build_id.build_id(("-DMOPS_OTHER",))
+
+
+def test_remove_nan_cpp_driver_compiles(engine_lib, tmp_path):
+    """tests/cpp/remove_nan_api.cpp (the GPU test's C++ API driver) builds against the header and
+    links against libmops_traj.so without a GPU."""
+    import shutil
+    import subprocess
+    if shutil.which("g++") is None:
+        pytest.skip("no g++")
+    libdir = os.path.join(ROOT, "mops_amd", "lib")
+    exe = str(tmp_path / "remove_nan_api")
+    subprocess.run(["g++", "-O2", "-std=c++17", "-Wall", "-Werror", "-I" + os.path.join(ROOT, "include"),
+                    os.path.join(ROOT, "tests", "cpp", "remove_nan_api.cpp"), "-L" + libdir, "-lmops_traj",
+                    "-Wl,-rpath," + libdir, "-Wl,-rpath-link,/opt/rocm/lib", "-o", exe], check=True)
+    assert os.path.exists(exe)

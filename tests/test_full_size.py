@@ -76,6 +76,29 @@ def _check_shells(lines, death):
     assert (r - r[:, :1]).abs().max().item() < 1e3
 
 
+@pytest.mark.parametrize("method", [1, 0], ids=["euler", "rk4"])
+def test_config1_lattice_every_line(ec_case, oracle_lib, method):
+    """BASELINE config 1: the 100-seed GenerateSamplePoint lattice (11 x 11 request, exclusive upper
+    bounds, lat [-40, 40], lon [-60, 60]) at "layer 10" (mid-depth of 0-based layer 10), dt 120 s,
+    1-day streamline, through the host drop-in (mops_run_trajectories): every line bit-exact."""
+    import bench
+    from mops_amd import synth
+    from mops_amd.engine import TrajectoryConfig, run_trajectories
+    mesh, dm, f0, _, r0, _ = ec_case
+    seeds = synth.lattice_seeds(11, 11, (-40.0, 40.0), (-60.0, 60.0))
+    assert len(seeds) == 100
+    depth = bench.layer_mid_depth(mesh, 10)
+    cfg = TrajectoryConfig(deltaT=120, simulationDuration=86400, recordT=3600, depth=depth, method=method)
+    got = run_trajectories(dm, f0, None, cfg, seeds)
+    ref = oracle_lib.run(mesh, r0, None, seeds, depth=depth, delta_t=120, duration=86400, record_t=3600,
+                         euler=(method == 1))
+    assert np.array_equal(got["cells"], ref["cells"])  # seed location = the oracle's exact 1-NN
+    assert np.array_equal(got["death_step"], ref["death"])
+    for k in ("points", "velocity", "lastPoint"):
+        assert np.array_equal(got[k], ref[k]), k
+    assert np.array_equal(got["final_depth"], ref["final_depth"])
+
+
 def test_config2_full_size(ec_case, oracle_lib):
     """BASELINE config 2: 1e6 particles, depth 800 m, dt 120 s, 1-day Euler streamline."""
     import torch

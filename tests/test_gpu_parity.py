@@ -275,6 +275,50 @@ def test_pipelined_advance_equals_single(gpu, dev_small, small_case):
             assert torch.equal(getattr(a, k), getattr(b, k)), k
 
 
+@pytest.mark.parametrize("back_on,method", [(False, 0), (True, 0), (False, 1)], ids=["sr", "pr", "se"])
+def test_dead_particle_compaction_is_result_invariant(gpu, dev_small, small_case, oracle_lib, back_on, method):
+    """Dead-particle compaction (advance_pipelined(compact=True): each part re-sorted with its dead
+    particles last before every chunk, records already written permuted along) leaves every line,
+    death step and final state bit-identical to one plain launch -- with RK4's Q1 deaths happening
+    throughout the run -- and puts each part's dead particles after its live ones."""
+    import torch
+    from mops_amd import synth
+    from mops_amd.engine import ParticleSet, TrajectoryConfig
+    mesh, s0, s1 = small_case
+    dm, f0, f1 = dev_small
+    back = f1 if back_on else None
+    seeds = synth.uniform_band_seeds(4099, seed=23)
+    cfg = TrajectoryConfig(deltaT=300, simulationDuration=86400, recordT=3600, depth=250.0, method=method)
+    a = ParticleSet(dm, seeds, 250.0, cfg)
+    a.advance(f0, back, 0, cfg.n_steps)
+    la = a.finalize(pathline=back_on)
+    b = ParticleSet(dm, seeds, 250.0, cfg)
+    streams = [torch.cuda.Stream() for _ in range(2)]
+    for st in streams:
+        st.wait_stream(torch.cuda.current_stream())
+    b.advance_pipelined(f0, back, 0, cfg.n_steps, streams, 7, compact=True)
+    for st in streams:
+        torch.cuda.current_stream().wait_stream(st)
+    lb = b.finalize(pathline=back_on)
+    torch.cuda.synchronize()
+    for k in ("points", "velocity", "temperature", "salinity", "lastPoint"):
+        assert torch.equal(la[k], lb[k]), k
+    for k in ("x", "y", "z", "depth", "cell", "death"):
+        assert torch.equal(a.original(getattr(a, k)), b.original(getattr(b, k))), k
+    death = b.original(b.death).cpu().numpy()
+    if method == 0:
+        assert (death >= 0).sum() > 50 and (death > 0).any()  # Q1 deaths during the run
+    # the oracle agrees on a sample (the compaction moved dead particles between waves)
+    r0 = oracle_lib.preprocess(mesh, s0)
+    r1 = oracle_lib.preprocess(mesh, s1) if back_on else None
+    idx = np.unique(np.concatenate([np.arange(0, 4099, 37), np.flatnonzero(death >= 0)[:40]]))
+    # seed cells: the oracle's own exact 1-NN (= mops_locate_cells, test_locate_matches_bruteforce)
+    ref = oracle_lib.run(mesh, r0, r1, seeds[idx], depth=250.0, delta_t=300, duration=86400, record_t=3600,
+                         euler=(method == 1))
+    assert np.array_equal(lb["points"][torch.as_tensor(idx, device=gpu)].cpu().numpy(), ref["points"])
+    assert np.array_equal(death[idx], ref["death"])
+
+
 def test_medium_mesh_l60_parity(gpu, engine_lib, medium_case, oracle_lib):
     """EC30to60-like vertical grid (60 levels): exercises the streaming bracket."""
     from mops_amd import synth

@@ -143,3 +143,28 @@ def test_preprocessing_boundary_vertices_zero(oracle_lib, small_case):
     assert np.all(d.vertex_ztop.reshape(-1, L)[bnd] == 0.0)
     assert np.all(d.vertex_vel.reshape(-1, L, 3)[bnd] == 0.0)
     assert np.all(np.diff(d.vertex_ztop.reshape(-1, L)[~bnd], axis=1) < 0)
+
+
+def test_config1_plumbing_on_the_oracle(oracle_lib):
+    """BASELINE config 1 on the CPU path (the reference's TBB plumbing case, no GPU): EC30to60-class
+    mesh, the 100-seed lattice at layer 10, dt 120 s, 1-day streamline, Euler and RK4.  Shapes and
+    record semantics of the assembled lines; RK4's Q1 deaths outnumber Euler's; every live line stays
+    on its shell.  (The GPU path reproduces these lines bit for bit: test_full_size.py.)"""
+    import bench
+    from mops_amd import synth
+    mesh = synth.make_mesh(158, n_levels=60)
+    d = oracle_lib.preprocess(mesh, synth.make_snapshot(mesh))
+    seeds = synth.lattice_seeds(11, 11, (-40.0, 40.0), (-60.0, 60.0))
+    depth = bench.layer_mid_depth(mesh, 10)
+    dead = {}
+    for euler in (True, False):
+        r = oracle_lib.run(mesh, d, None, seeds, depth=depth, delta_t=120, duration=86400, record_t=3600,
+                           euler=euler)
+        assert r["points"].shape == (100, 25, 3) and r["velocity"].shape == (100, 25, 3)
+        assert np.array_equal(r["points"][:, 0], seeds)                    # line = [seed] + 24 records
+        assert np.all(r["velocity"][:, -1] == 0.0)                         # the appended zero velocity
+        live = r["death"] < 0
+        rad = np.linalg.norm(r["points"][live], axis=-1)
+        assert np.all(np.abs(rad - rad[:, :1]) < 1e3)
+        dead[euler] = int((~live).sum())
+    assert dead[False] > dead[True]
