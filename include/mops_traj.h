@@ -69,6 +69,9 @@ typedef struct {
     const double* h_zonal_velocity;      /* cellZonalVelocity_vec [C*L] */
     const double* h_meridional_velocity; /* cellMeridionalVelocity_vec [C*L] */
     const double* h_vert_velocity_top;   /* cellVertVelocity_vec [C*(L+1)] or NULL (= 0) */
+    const double* h_normal_velocity;     /* cellNormalVelocity_vec [E*L] or NULL: used only when the
+                                            zonal/meridional pair is absent, on a mesh with edges
+                                            (mops_mesh_set_edges) -- the RBF reconstruction */
 } mops_snapshot_desc;
 
 /* TrajectorySettings (src/Core/MPASOVisualizer.h:90-103); seconds. */
@@ -115,11 +118,31 @@ void mops_mesh_destroy(mops_mesh* mesh);
 /* Bytes the mesh occupies in HBM. */
 int64_t mops_mesh_bytes(const mops_mesh* mesh);
 
+/* Upload the mesh's edges (MPASOGrid edgesOnCell_vec [C*maxE], cellsOnEdge_vec
+ * [E*2], edgeCoord_vec [E*3], reference storage form) for the RBF
+ * reconstruction of the cell-centre velocity from edge-normal velocities
+ * (TBBBackend::CalcCellCenterVelocity, src/CPU/TBB/MPASOSolutionTBB.cpp:131-245,
+ * reached through MPASOSolution::calcCellCenterVelocity,
+ * src/Core/MPASOSolution.cpp:85-110).  The per-cell RBF systems depend on the
+ * geometry only and are solved here once.  MOPS_ERR_UNSUPPORTED if a cell has
+ * more than 7 edges (the reference's stencil arrays hold MAX_VERTEX_NUM = 7). */
+mops_status mops_mesh_set_edges(mops_mesh* mesh, int64_t n_edges, const uint64_t* h_edges_on_cell,
+                                const uint64_t* h_cells_on_edge, const double* h_edge_coord, void* stream);
+/* The RBF cell-centre velocity [C*L*3] from the edge-normal velocity [E*L]
+ * (device pointers) -- TBBBackend::CalcCellCenterVelocity's output, bit for
+ * bit, quirks included: the stencil always has 7 points (absent edges enter
+ * as zero points with zero unit vectors, which makes the 7x7 system singular,
+ * i.e. NaN, for every cell with fewer than 7 edges), alpha is 1 and the
+ * right-hand side evaluates the RBF at 1 (Interpolation.hpp:223-302). */
+mops_status mops_cell_center_velocity_rbf(const mops_mesh* mesh, const double* d_normal_velocity, double* d_out,
+                                          void* stream);
+
 /* Upload raw fields and derive, on the GPU, the vertex arrays the trajectory
  * kernels read.  Replaces MOPSApp::addSol's preprocessing chain
  * (src/Core/MOPSApp.cpp:100-129): MPASOSolution::calcCellCenterZtop
  * (MPASOSolution.cpp:535-618), TBBBackend::CalcCellVertexZtop
- * (MPASOSolutionTBB.cpp:9-55), CalcCellCenterVelocityByZM (:108-129),
+ * (MPASOSolutionTBB.cpp:9-55), CalcCellCenterVelocityByZM (:108-129) -- or,
+ * for a snapshot with edge normals only, CalcCellCenterVelocity (:131-245),
  * CalcCellVertexVelocity (:270-318), CalcCellVertexVertVelocity (:320-366). */
 mops_status mops_field_create(const mops_mesh* mesh, const mops_snapshot_desc* desc, void* stream,
                               mops_field** out);

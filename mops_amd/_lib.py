@@ -15,7 +15,7 @@ LIB_PATH = os.path.join(_HERE, "lib", "libmops_traj.so")
 # every symbol include/mops_traj.h declares (checked by tests/test_abi.py)
 EXPORTED = (
     "mops_last_error", "mops_abi_version", "mops_selftest_math",
-    "mops_mesh_create", "mops_mesh_destroy", "mops_mesh_bytes",
+    "mops_mesh_create", "mops_mesh_destroy", "mops_mesh_bytes", "mops_mesh_set_edges", "mops_cell_center_velocity_rbf",
     "mops_field_create", "mops_field_create_device", "mops_field_rebuild_device", "mops_field_create_derived", "mops_field_export", "mops_cell_to_vertex_attr",
     "mops_field_destroy", "mops_field_bytes",
     "mops_locate_cells", "mops_locate_cells_hinted", "mops_order_particles", "mops_order_scratch_bytes",
@@ -44,7 +44,8 @@ class MeshDesc(C.Structure):
 class SnapshotDesc(C.Structure):
     _fields_ = [("timestep", C.c_int32), ("h_layer_thickness", C.c_void_p), ("h_bottom_depth", C.c_void_p),
                 ("h_surface_height", C.c_void_p), ("h_zonal_velocity", C.c_void_p),
-                ("h_meridional_velocity", C.c_void_p), ("h_vert_velocity_top", C.c_void_p)]
+                ("h_meridional_velocity", C.c_void_p), ("h_vert_velocity_top", C.c_void_p),
+                ("h_normal_velocity", C.c_void_p)]
 
 
 class TrajCfg(C.Structure):
@@ -103,6 +104,8 @@ def load(path: str | None = None):
     lib.mops_mesh_create.argtypes = [P, P, P]; lib.mops_mesh_create.restype = st
     lib.mops_mesh_destroy.argtypes = [P]; lib.mops_mesh_destroy.restype = None
     lib.mops_mesh_bytes.argtypes = [P]; lib.mops_mesh_bytes.restype = I64
+    lib.mops_mesh_set_edges.argtypes = [P, I64, P, P, P, P]; lib.mops_mesh_set_edges.restype = st
+    lib.mops_cell_center_velocity_rbf.argtypes = [P, P, P, P]; lib.mops_cell_center_velocity_rbf.restype = st
     lib.mops_field_create.argtypes = [P, P, P, P]; lib.mops_field_create.restype = st
     lib.mops_field_create_device.argtypes = [P, P, P, P]; lib.mops_field_create_device.restype = st
     lib.mops_field_rebuild_device.argtypes = [P, P, P]; lib.mops_field_rebuild_device.restype = st

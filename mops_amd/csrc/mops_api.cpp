@@ -90,6 +90,7 @@ mops_field* make_field(const MPASOSolution& s) {
     d.h_zonal_velocity = s.cellZonalVelocity_vec.empty() ? nullptr : s.cellZonalVelocity_vec.data();
     d.h_meridional_velocity = s.cellMeridionalVelocity_vec.empty() ? nullptr : s.cellMeridionalVelocity_vec.data();
     d.h_vert_velocity_top = s.cellVertVelocity_vec.empty() ? nullptr : s.cellVertVelocity_vec.data();
+    d.h_normal_velocity = s.cellNormalVelocity_vec.empty() ? nullptr : s.cellNormalVelocity_vec.data();
     mops_field* f = nullptr;
     check(mops_field_create(g_app.mesh, &d, nullptr, &f), "mops_field_create");
     return f;
@@ -302,6 +303,18 @@ void MOPS_End() {
     d.h_vertex_coord = reinterpret_cast<const double*>(g.vertexCoord_vec.data());
     g_app.release();
     check(mops_mesh_create(&d, nullptr, &g_app.mesh), "mops_mesh_create");
+    // a solution with edge-normal velocity only (AttributeType::kNormalVelocity) is reconstructed by
+    // the RBF path (MPASOSolution::calcCellCenterVelocity), which needs the mesh's edges
+    bool rbf = false;
+    for (auto& kv : g_app.sols)
+        rbf = rbf || ((kv.second->cellZonalVelocity_vec.empty() || kv.second->cellMeridionalVelocity_vec.empty()) &&
+                      !kv.second->cellNormalVelocity_vec.empty());
+    if (rbf)
+        check(mops_mesh_set_edges(g_app.mesh, (int64_t)g.edgeCoord_vec.size(),
+                                  reinterpret_cast<const uint64_t*>(g.edgesOnCell_vec.data()),
+                                  reinterpret_cast<const uint64_t*>(g.cellsOnEdge_vec.data()),
+                                  reinterpret_cast<const double*>(g.edgeCoord_vec.data()), nullptr),
+              "mops_mesh_set_edges");
     for (auto& kv : g_app.sols) g_app.fields[kv.first] = make_field(*kv.second);
     if (!g_app.fields.empty()) g_app.front = g_app.fields.begin()->second;  // addField: first map entry
 }

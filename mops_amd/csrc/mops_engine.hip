@@ -102,6 +102,14 @@ struct mops_mesh {
     mutable void* d_scratch = nullptr;
     mutable size_t scratch_bytes = 0;
     int64_t bytes = 0;
+    std::vector<int> h_nv;  // nEdgesOnCell (host copy, for mops_mesh_set_edges' validation)
+    // edges (mops_mesh_set_edges): the RBF reconstruction's per-cell stencil, solved once
+    int64_t E = 0;
+    int* d_eoc = nullptr;        // [C][7] edgesOnCell 0-based, -1 = none
+    int2* d_coe = nullptr;       // [E] cellsOnEdge 0-based, -1 = none (the reference's SIZE_MAX)
+    double4* d_exyz = nullptr;   // [E] edgeCoord
+    double* d_rbf_coef = nullptr;  // [C][7][3] RBF coefficients (rbf_coef_kernel)
+    int* d_rbf_slot = nullptr;     // [C][7] edge read by each slot, -1 = velocity 0
 };
 
 struct mops_field {
@@ -1542,6 +1550,158 @@ __global__ void center_vel_zm_kernel(int64_t C, int L, const double4* cxyz, cons
     o[2] = clat * um + slat * uu;
 }
 
+// ---------------------------------------------------------------------------
+// RBF reconstruction of the cell-centre velocity from edge normals
+// (TBBBackend::CalcCellCenterVelocity, MPASOSolutionTBB.cpp:131-245, with
+// Interpolator::mpas_rbf_interp_func_3D_plane_vec_const_dir_comp_coeffs and
+// gauss_elimination_fixed, Interpolation.hpp:167-340).  The reference solves
+// the same two 7x7 systems for every (cell, layer); they depend on the cell's
+// geometry only, so the engine solves them once per cell when the mesh's edges
+// are uploaded (rbf_coef_kernel, same operations in the same order) and each
+// snapshot's derivation is the reference's final 7-term sums per (cell,
+// layer) (rbf_apply_kernel).  Quirks kept: pointCount is always
+// MAX_VERTEX_NUM = 7 (absent edges are zero points with zero unit vectors,
+// which makes the system singular -- NaN -- for every cell with fewer than 7
+// edges), alpha is forced to 1 and the right-hand side evaluates the RBF at 1.
+// ---------------------------------------------------------------------------
+constexpr int kRbfN = 7;
+
+__device__ __forceinline__ void rbf_gauss7(double (&A)[8][8], double (&b)[8], double (&x)[8]) {
+    int pivot[8];
+#pragma unroll
+    for (int i = 0; i < kRbfN; i++) pivot[i] = i;
+    for (int j = 0; j < kRbfN - 1; ++j) {
+        int maxRow = j;
+        for (int i = j + 1; i < kRbfN; ++i)
+            if (fabs(A[pivot[i]][j]) > fabs(A[pivot[maxRow]][j])) maxRow = i;
+        const int tmp = pivot[j]; pivot[j] = pivot[maxRow]; pivot[maxRow] = tmp;
+        for (int i = j + 1; i < kRbfN; ++i) {
+            const double factor = A[pivot[i]][j] / A[pivot[j]][j];
+            A[pivot[i]][j] = factor;
+            for (int k = j + 1; k < kRbfN; ++k) A[pivot[i]][k] -= factor * A[pivot[j]][k];
+            b[pivot[i]] -= factor * b[pivot[j]];
+        }
+    }
+    x[kRbfN - 1] = b[pivot[kRbfN - 1]] / A[pivot[kRbfN - 1]][kRbfN - 1];
+    for (int i = kRbfN - 2; i >= 0; --i) {
+        double sum = 0.0;
+        for (int j = i + 1; j < kRbfN; ++j) sum += A[pivot[i]][j] * x[j];
+        x[i] = (b[pivot[i]] - sum) / A[pivot[i]][i];
+    }
+}
+
+// one thread per cell: coef [C][7][3] and the 7 edge ids (-1 = the slot's velocity is 0)
+__global__ void __launch_bounds__(64) rbf_coef_kernel(int64_t C, int rec_ints, const int* __restrict__ cellrec,
+                                                      const int* __restrict__ eoc, const int2* __restrict__ coe,
+                                                      const double4* __restrict__ exyz,
+                                                      const double4* __restrict__ cxyz, double* __restrict__ coef,
+                                                      int* __restrict__ slot_edge) {
+    const int64_t c = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (c >= C) return;
+    const double4 p = cxyz[c];
+    const int nv = cellrec[c * rec_ints];
+    const double pl = sqrt(p.x * p.x + p.y * p.y + p.z * p.z);
+    const double ux = p.x / pl, uy = p.y / pl, uz = p.z / pl;                          // up
+    double ex = 0.0 * uz - 1.0 * uy, ey = 1.0 * ux - 0.0 * uz, ez = 0.0 * uy - 0.0 * ux;  // (0,0,1) x up
+    if (sqrt(ex * ex + ey * ey + ez * ez) < 1e-6) {
+        ex = 1.0 * uz - 0.0 * uy; ey = 0.0 * ux - 0.0 * uz; ez = 0.0 * uy - 1.0 * ux;      // (0,1,0) x up
+    }
+    const double el = sqrt(ex * ex + ey * ey + ez * ez);
+    ex = ex / el; ey = ey / el; ez = ez / el;
+    const double nx = uy * ez - uz * ey, ny = uz * ex - ux * ez, nz = ux * ey - uy * ex;  // up x east
+    const double pb[2][3] = {{ex, ey, ez}, {nx, ny, nz}};
+    double ps[8][2], pu[8][2];
+    int sl[8];
+#pragma unroll
+    for (int s = 0; s < kRbfN; ++s) {
+        double e0 = 0.0, e1 = 0.0, e2 = 0.0, n0 = 0.0, n1 = 0.0, n2 = 0.0;
+        int e = (s < nv) ? eoc[c * kRbfN + s] : -1;
+        if (e >= 0) {
+            const double4 ep = exyz[e];
+            e0 = ep.x; e1 = ep.y; e2 = ep.z;
+            const int2 ce = coe[e];  // 0-based, -1 = none (the reference's SIZE_MAX)
+            const uint64_t c0 = (uint64_t)(int64_t)ce.x, c1 = (uint64_t)(int64_t)ce.y;
+            const uint64_t lo = c0 < c1 ? c0 : c1, hi = c0 > c1 ? c0 : c1;
+            double vx, vy, vz;
+            const double4 a = cxyz[lo];
+            if (hi > (uint64_t)C) {
+                vx = ep.x - a.x; vy = ep.y - a.y; vz = ep.z - a.z;
+            } else {
+                const double4 b = cxyz[hi];
+                vx = b.x - a.x; vy = b.y - a.y; vz = b.z - a.z;
+            }
+            const double l = sqrt(vx * vx + vy * vy + vz * vz);
+            if (l == 0.0) {
+                e = -1;  // skipped: the slot keeps its edge centre, zero unit vector and zero velocity
+            } else {
+                n0 = vx / l; n1 = vy / l; n2 = vz / l;
+            }
+            // (the reference records the edge centre before the length test)
+        }
+        sl[s] = e;
+        ps[s][0] = e0 * pb[0][0] + e1 * pb[0][1] + e2 * pb[0][2];
+        ps[s][1] = e0 * pb[1][0] + e1 * pb[1][1] + e2 * pb[1][2];
+        pu[s][0] = n0 * pb[0][0] + n1 * pb[0][1] + n2 * pb[0][2];
+        pu[s][1] = n0 * pb[1][0] + n1 * pb[1][1] + n2 * pb[1][2];
+    }
+    double A[8][8], rhs[8][2];
+    const double rvd = 1.0 / sqrt(1.0 + 1.0);  // evaluate_rbf(1.0)
+    for (int j = 0; j < kRbfN; ++j) {
+        for (int i = j; i < kRbfN; ++i) {
+            double r2 = 0.0;
+            double diff = ps[i][0] - ps[j][0];
+            r2 += diff * diff;
+            diff = ps[i][1] - ps[j][1];
+            r2 += diff * diff;
+            r2 /= (1.0 * 1.0);
+            const double rv = 1.0 / sqrt(1.0 + r2);
+            const double dp = pu[i][0] * pu[j][0] + pu[i][1] * pu[j][1];
+            A[i][j] = rv * dp;
+            A[j][i] = A[i][j];
+        }
+        rhs[j][0] = rvd * pu[j][0];
+        rhs[j][1] = rvd * pu[j][1];
+    }
+    double Ac[8][8], b[8], x1[8], x2[8];
+    for (int i = 0; i < kRbfN; ++i)
+        for (int j = 0; j < kRbfN; ++j) Ac[i][j] = A[i][j];
+    for (int i = 0; i < kRbfN; ++i) b[i] = rhs[i][0];
+    rbf_gauss7(Ac, b, x1);
+    for (int i = 0; i < kRbfN; ++i)
+        for (int j = 0; j < kRbfN; ++j) Ac[i][j] = A[i][j];
+    for (int i = 0; i < kRbfN; ++i) b[i] = rhs[i][1];
+    rbf_gauss7(Ac, b, x2);
+    for (int i = 0; i < kRbfN; ++i) {
+        double* o = coef + (c * kRbfN + i) * 3;
+        o[0] = pb[0][0] * x1[i] + pb[1][0] * x2[i];
+        o[1] = pb[0][1] * x1[i] + pb[1][1] * x2[i];
+        o[2] = pb[0][2] * x1[i] + pb[1][2] * x2[i];
+        slot_edge[c * kRbfN + i] = sl[i];
+    }
+}
+
+// one thread per (cell, layer): the reference's 7-term sums (:234-243); a slot without an edge
+// (or with a zero-length normal) contributes coef * 0.0, as in the reference
+__global__ void rbf_apply_kernel(int64_t C, int L, const double* __restrict__ coef, const int* __restrict__ slot_edge,
+                                 const double* __restrict__ normal_vel, double* __restrict__ out) {
+    const int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (idx >= C * L) return;
+    const int64_t c = idx / L;
+    const int k = (int)(idx - c * L);
+    double xv = 0.0, yv = 0.0, zv = 0.0;
+#pragma unroll
+    for (int s = 0; s < kRbfN; ++s) {
+        const int e = slot_edge[c * kRbfN + s];
+        const double nv = (e >= 0) ? normal_vel[(int64_t)e * L + k] : 0.0;
+        const double* q = coef + (c * kRbfN + s) * 3;
+        xv += q[0] * nv;
+        yv += q[1] * nv;
+        zv += q[2] * nv;
+    }
+    double* o = out + 3 * idx;
+    o[0] = xv; o[1] = yv; o[2] = zv;
+}
+
 // CalcCellVertexZtop / CenterToVertex / VertexVelocity / VertexVertVelocity
 // (MPASOSolutionTBB.cpp:9-106, 270-366): barycentric of the 3 cellsOnVertex.
 template <int DIM>
@@ -2036,6 +2196,8 @@ void free_mesh(mops_mesh* m) {
     (void)hipFree(m->d_cellrec); (void)hipFree(m->d_cxyz); (void)hipFree(m->d_vxyz); (void)hipFree(m->d_cov);
     (void)hipFree(m->d_bkeys); (void)hipFree(m->d_bcells); (void)hipFree(m->d_hkeys); (void)hipFree(m->d_hval); (void)hipFree(m->d_cell_key); (void)hipFree(m->d_cellB); (void)hipFree(m->d_rloc2); (void)hipFree(m->d_ring);
     (void)hipFree(m->d_scratch);
+    (void)hipFree(m->d_eoc); (void)hipFree(m->d_coe); (void)hipFree(m->d_exyz); (void)hipFree(m->d_rbf_coef);
+    (void)hipFree(m->d_rbf_slot);
     delete m;
 }
 
@@ -2136,11 +2298,13 @@ mops_status mops_mesh_create(const mops_mesh_desc* desc, void* stream, mops_mesh
     m->rec_ints = rec_ints_for(m->maxv);
     // ---- cell records (validated) ----
     std::vector<int> rec((size_t)C * m->rec_ints, -1);
+    m->h_nv.reserve((size_t)C);
     for (int64_t c = 0; c < C; ++c) {
         const uint64_t ne = desc->h_n_edges_on_cell[c];
         if (ne > (uint64_t)maxE) { free_mesh(m); return fail(MOPS_ERR_INVALID, "nEdgesOnCell > maxEdges"); }
         int* r = rec.data() + c * m->rec_ints;
         r[0] = (int)ne;
+        m->h_nv.push_back((int)ne);
         for (int k = 0; k < maxE; ++k) {
             const uint64_t v1 = desc->h_vertices_on_cell[c * maxE + k];
             const uint64_t c1 = desc->h_cells_on_cell[c * maxE + k];
@@ -2279,6 +2443,76 @@ mops_status mops_mesh_create(const mops_mesh_desc* desc, void* stream, mops_mesh
 void mops_mesh_destroy(mops_mesh* mesh) { free_mesh(mesh); }
 int64_t mops_mesh_bytes(const mops_mesh* mesh) { return mesh ? mesh->bytes : 0; }
 
+mops_status mops_mesh_set_edges(mops_mesh* m, int64_t n_edges, const uint64_t* h_edges_on_cell,
+                                const uint64_t* h_cells_on_edge, const double* h_edge_coord, void* stream) {
+    if (!m || n_edges <= 0 || n_edges >= INT32_MAX || !h_edges_on_cell || !h_cells_on_edge || !h_edge_coord)
+        return fail(MOPS_ERR_INVALID, "mops_mesh_set_edges: invalid argument");
+    if (m->d_eoc) return fail(MOPS_ERR_INVALID, "mops_mesh_set_edges: the mesh already has edges");
+    const int64_t C = m->C, E = n_edges;
+    const int maxE = m->maxE;
+    // cellsOnEdge, 0-based; -1 = the reference's "max_cell_id > CELL_SIZE" side (id 0, or id - 1 > C)
+    std::vector<int2> coe((size_t)E);
+    for (int64_t e = 0; e < E; ++e) {
+        int v[2];
+        for (int j = 0; j < 2; ++j) {
+            const uint64_t x = h_cells_on_edge[2 * e + j];
+            if (x >= 1 && x <= (uint64_t)C) v[j] = (int)(x - 1);
+            else if (x == (uint64_t)C + 1) return fail(MOPS_ERR_INVALID, "cellsOnEdge entry C+1 (reference reads out of range)");
+            else v[j] = -1;
+        }
+        coe[(size_t)e] = make_int2(v[0], v[1]);
+    }
+    std::vector<int> eoc((size_t)C * kRbfN, -1);
+    for (int64_t c = 0; c < C; ++c) {
+        const int nv = m->h_nv[(size_t)c];
+        if (nv > kRbfN)
+            return fail(MOPS_ERR_UNSUPPORTED, "mops_mesh_set_edges: a cell with more than 7 edges (the reference's RBF "
+                                              "stencil holds MAX_VERTEX_NUM = 7, MPASOSolutionTBB.cpp:142)");
+        for (int k = 0; k < nv; ++k) {
+            const uint64_t x = h_edges_on_cell[c * maxE + k];
+            if (x == 0) continue;  // the reference skips it (edge id SIZE_MAX)
+            if (x > (uint64_t)E) return fail(MOPS_ERR_INVALID, "edgesOnCell entry out of range");
+            const int e = (int)(x - 1);
+            if (coe[(size_t)e].x < 0 && coe[(size_t)e].y < 0)
+                return fail(MOPS_ERR_INVALID, "an edge of a cell has no valid cellsOnEdge entry (reference reads "
+                                              "cellCoord[SIZE_MAX])");
+            eoc[(size_t)(c * kRbfN + k)] = e;
+        }
+    }
+    hipStream_t s = (hipStream_t)stream;
+    int64_t acc = 0;
+    mops_status st;
+    if ((st = upload(eoc.data(), eoc.size(), &m->d_eoc, &acc, s)) != MOPS_OK ||
+        (st = upload(coe.data(), coe.size(), &m->d_coe, &acc, s)) != MOPS_OK ||
+        (st = upload_xyz(h_edge_coord, E, &m->d_exyz, &acc, s)) != MOPS_OK ||
+        (st = dmalloc(&m->d_rbf_coef, (size_t)(C * kRbfN * 3), &acc)) != MOPS_OK ||
+        (st = dmalloc(&m->d_rbf_slot, (size_t)(C * kRbfN), &acc)) != MOPS_OK) {
+        (void)hipFree(m->d_eoc); (void)hipFree(m->d_coe); (void)hipFree(m->d_exyz); (void)hipFree(m->d_rbf_coef);
+        (void)hipFree(m->d_rbf_slot);
+        m->d_eoc = nullptr; m->d_coe = nullptr; m->d_exyz = nullptr; m->d_rbf_coef = nullptr; m->d_rbf_slot = nullptr;
+        return st;
+    }
+    rbf_coef_kernel<<<(unsigned)((C + 63) / 64), 64, 0, s>>>(C, m->rec_ints, m->d_cellrec, m->d_eoc, m->d_coe,
+                                                             m->d_exyz, m->d_cxyz, m->d_rbf_coef, m->d_rbf_slot);
+    HIP_TRY(hipGetLastError());
+    HIP_TRY(hipStreamSynchronize(s));
+    m->E = E;
+    m->bytes += acc;
+    return MOPS_OK;
+}
+
+mops_status mops_cell_center_velocity_rbf(const mops_mesh* m, const double* d_normal_velocity, double* d_out,
+                                          void* stream) {
+    if (!m || !d_normal_velocity || !d_out) return fail(MOPS_ERR_INVALID, "mops_cell_center_velocity_rbf: null argument");
+    if (!m->d_rbf_coef) return fail(MOPS_ERR_INVALID, "mops_cell_center_velocity_rbf: the mesh has no edges "
+                                                      "(mops_mesh_set_edges)");
+    const int64_t n = m->C * (int64_t)m->L;
+    rbf_apply_kernel<<<grid_for(n), kBlock, 0, (hipStream_t)stream>>>(m->C, m->L, m->d_rbf_coef, m->d_rbf_slot,
+                                                                      d_normal_velocity, d_out);
+    HIP_TRY(hipGetLastError());
+    return MOPS_OK;
+}
+
 static mops_status compute_mono(const mops_mesh* mesh, mops_field* f, hipStream_t s) {
     const int64_t npr = mesh->V * (int64_t)std::max(mesh->L - 1, 0);
     // + one all-zero record at index npr: pair_sums reads it for v >= nv
@@ -2364,8 +2598,9 @@ mops_status mops_field_rebuild_device(mops_field* field, const mops_snapshot_des
 static mops_status check_snapshot(const mops_mesh* mesh, const mops_snapshot_desc* desc) {
     if (!desc->h_layer_thickness)
         return fail(MOPS_ERR_INVALID, "cellLayerThickness is not defined");  // MPASOSolution.cpp:540-544
-    if (!desc->h_zonal_velocity || !desc->h_meridional_velocity)
-        return fail(MOPS_ERR_INVALID, "zonal/meridional velocity required");
+    const bool zm = desc->h_zonal_velocity && desc->h_meridional_velocity;
+    if (!zm && !(desc->h_normal_velocity && mesh->d_rbf_coef))
+        return fail(MOPS_ERR_INVALID, "zonal/meridional velocity (or normalVelocity on a mesh with edges) required");
     if (!mesh->d_cov) return fail(MOPS_ERR_INVALID, "mesh has no cellsOnVertex");
     return MOPS_OK;
 }
@@ -2387,8 +2622,12 @@ static mops_status field_derive(const mops_mesh* mesh, mops_field* f, const mops
     cell_ztop_kernel<<<grid_for(C), kBlock, 0, s>>>(C, L, d->h_layer_thickness, bot, ssh, ztc);
     cell_to_vertex_kernel<1><<<grid_for(V * L), kBlock, 0, s>>>(V, L, mesh->d_cov, mesh->d_cxyz, mesh->d_vxyz, ztc,
                                                                f->d_zt, 0);
-    center_vel_zm_kernel<<<grid_for(C * L), kBlock, 0, s>>>(C, L, mesh->d_cxyz, d->h_zonal_velocity,
-                                                            d->h_meridional_velocity, velc);
+    if (d->h_zonal_velocity && d->h_meridional_velocity) {  // the live path (MOPSApp.cpp:113)
+        center_vel_zm_kernel<<<grid_for(C * L), kBlock, 0, s>>>(C, L, mesh->d_cxyz, d->h_zonal_velocity,
+                                                                d->h_meridional_velocity, velc);
+    } else {  // edge normals only: the RBF reconstruction (MPASOSolution::calcCellCenterVelocity)
+        MOPS_TRY(mops_cell_center_velocity_rbf(mesh, d->h_normal_velocity, velc, s));
+    }
     cell_to_vertex_kernel<3><<<grid_for(V * L), kBlock, 0, s>>>(V, L, mesh->d_cov, mesh->d_cxyz, mesh->d_vxyz, velc,
                                                                f->d_vel, 0);
     if (d->h_vert_velocity_top) {
@@ -2417,6 +2656,7 @@ static mops_status field_create_impl(const mops_mesh* mesh, const mops_snapshot_
     f->mesh = mesh; f->V = mesh->V; f->L = L;
     mops_snapshot_desc dd = *desc;  // device view of the raw arrays
     double *thick = nullptr, *bot = nullptr, *ssh = nullptr, *zon = nullptr, *mer = nullptr, *wc = nullptr;
+    double* nrm = nullptr;
     double *ztc = nullptr, *velc = nullptr;
     int64_t scratch = 0;
     mops_status st = MOPS_OK;
@@ -2427,12 +2667,17 @@ static mops_status field_create_impl(const mops_mesh* mesh, const mops_snapshot_
                 break;
             if (!desc->h_bottom_depth && desc->h_surface_height &&
                 (st = upload(desc->h_surface_height, (size_t)C, &ssh, &scratch, s)) != MOPS_OK) break;
-            if ((st = upload(desc->h_zonal_velocity, (size_t)(C * L), &zon, &scratch, s)) != MOPS_OK) break;
-            if ((st = upload(desc->h_meridional_velocity, (size_t)(C * L), &mer, &scratch, s)) != MOPS_OK) break;
+            if (desc->h_zonal_velocity && desc->h_meridional_velocity) {
+                if ((st = upload(desc->h_zonal_velocity, (size_t)(C * L), &zon, &scratch, s)) != MOPS_OK) break;
+                if ((st = upload(desc->h_meridional_velocity, (size_t)(C * L), &mer, &scratch, s)) != MOPS_OK) break;
+            } else if ((st = upload(desc->h_normal_velocity, (size_t)(mesh->E * L), &nrm, &scratch, s)) != MOPS_OK) {
+                break;
+            }
             if (desc->h_vert_velocity_top &&
                 (st = upload(desc->h_vert_velocity_top, (size_t)(C * (L + 1)), &wc, &scratch, s)) != MOPS_OK) break;
             dd.h_layer_thickness = thick; dd.h_bottom_depth = bot; dd.h_surface_height = ssh;
             dd.h_zonal_velocity = zon; dd.h_meridional_velocity = mer; dd.h_vert_velocity_top = wc;
+            dd.h_normal_velocity = nrm;
         }
         if ((st = dmalloc(&ztc, (size_t)(C * L), on_device ? &f->bytes : &scratch)) != MOPS_OK) break;
         if (on_device) f->d_ztc = ztc;  // owned by the field from here on
@@ -2444,7 +2689,7 @@ static mops_status field_create_impl(const mops_mesh* mesh, const mops_snapshot_
     } while (0);
     if (!on_device) {
         (void)hipFree(thick); (void)hipFree(bot); (void)hipFree(ssh); (void)hipFree(zon); (void)hipFree(mer);
-        (void)hipFree(wc); (void)hipFree(ztc); (void)hipFree(velc);
+        (void)hipFree(wc); (void)hipFree(nrm); (void)hipFree(ztc); (void)hipFree(velc);
     }
     if (st != MOPS_OK) { free_field(f); return st; }
     *out = f;

@@ -86,6 +86,16 @@ class DeviceMesh:
                    nEdgesOnCell=m.nEdgesOnCell, verticesOnCell=m.verticesOnCell, cellsOnCell=m.cellsOnCell,
                    cellsOnVertex=m.cellsOnVertex, cellCoord=m.cellCoord, vertexCoord=m.vertexCoord, stream=stream)
 
+    def set_edges(self, nEdges, edgesOnCell, cellsOnEdge, edgeCoord, stream=None):
+        """Upload the mesh's edges for the RBF velocity reconstruction (mops_mesh_set_edges)."""
+        eoc = np.ascontiguousarray(edgesOnCell, dtype=np.uint64)
+        coe = np.ascontiguousarray(cellsOnEdge, dtype=np.uint64)
+        ec = np.ascontiguousarray(edgeCoord, dtype=np.float64).reshape(-1)
+        L.check(L.load().mops_mesh_set_edges(self.handle, int(nEdges), _ptr(eoc), _ptr(coe), _ptr(ec),
+                                             _stream_handle(stream)), "mops_mesh_set_edges")
+        self.nEdges = int(nEdges)
+        return self
+
     @property
     def nbytes(self) -> int:
         return int(L.load().mops_mesh_bytes(self.handle))
@@ -121,11 +131,16 @@ class DeviceField:
         self.handle = handle
 
     @classmethod
-    def from_snapshot(cls, mesh: DeviceMesh, snap, stream=None):
+    def from_snapshot(cls, mesh: DeviceMesh, snap, stream=None, velocity: str = "zonal"):
+        """``velocity``: "zonal" -- the cell velocity from zonal/meridional components (the reference's
+        live path, MOPSApp.cpp:113); "rbf" -- reconstructed from ``snap.normalVelocity`` on the edges
+        (MPASOSolution::calcCellCenterVelocity; the mesh needs ``DeviceMesh.set_edges``)."""
         lib = L.load()
+        rbf = velocity == "rbf"
         keep = [np.ascontiguousarray(x, dtype=np.float64) if x is not None else None for x in
-                (snap.layerThickness, snap.bottomDepth, getattr(snap, "surfaceHeight", None), snap.zonalVelocity,
-                 snap.meridionalVelocity, snap.vertVelocityTop)]
+                (snap.layerThickness, snap.bottomDepth, getattr(snap, "surfaceHeight", None),
+                 None if rbf else snap.zonalVelocity, None if rbf else snap.meridionalVelocity, snap.vertVelocityTop,
+                 getattr(snap, "normalVelocity", None) if rbf else None)]
         desc = L.SnapshotDesc(int(snap.timestep), *[_ptr(x) for x in keep])
         h = C.c_void_p()
         L.check(lib.mops_field_create(mesh.handle, C.byref(desc), _stream_handle(stream), C.byref(h)),
@@ -142,7 +157,8 @@ class DeviceField:
                 raise ValueError(f"{k}: expected a contiguous float64 CUDA tensor")
             return C.c_void_p(t.data_ptr())
         return L.SnapshotDesc(int(timestep), dp("layerThickness"), dp("bottomDepth"), dp("surfaceHeight"),
-                              dp("zonalVelocity"), dp("meridionalVelocity"), dp("vertVelocityTop"))
+                              dp("zonalVelocity"), dp("meridionalVelocity"), dp("vertVelocityTop"),
+                              dp("normalVelocity"))
 
     @classmethod
     def from_device_snapshot(cls, mesh: DeviceMesh, snap: dict, timestep: int = 0, stream=None):

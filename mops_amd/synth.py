@@ -122,6 +122,12 @@ class Mesh:
     refBottomDepth: np.ndarray     # [L] float64 (m, positive down)
     lat_cell: np.ndarray           # [C] rad
     lon_cell: np.ndarray           # [C] rad
+    # edges (MPASOGrid edgesOnCell_vec / cellsOnEdge_vec / edgeCoord_vec): edge k of cell c lies
+    # between its vertices k and k+1 and is shared with cellsOnCell[c, k]
+    nEdges: int = 0
+    edgesOnCell: np.ndarray = None   # [C*maxEdges] uint64, 1-based, 0 padded
+    cellsOnEdge: np.ndarray = None   # [E*2] uint64, 1-based, 0 = culled (land) side
+    edgeCoord: np.ndarray = None     # [E,3] float64 (m): the edge midpoint on the sphere
 
     @property
     def nVertLevelsP1(self) -> int:
@@ -153,10 +159,56 @@ def _land_mask(lat, lon, kind: str):
     return m
 
 
+def _flip_edges(pts, T, n_flips: int, seed: int, max_deg: int):
+    """Flip ``n_flips`` interior diagonals of the triangulation (vertex-disjoint, convex quads only):
+    each turns two hexagonal Voronoi cells into pentagons and two into heptagons -- the 7-edge cells
+    real MPAS meshes have and icosahedral duals lack (the RBF reconstruction's 7-point stencil,
+    MPASOSolutionTBB.cpp:142, is only finite on them)."""
+    if n_flips <= 0:
+        return T
+    T = T.copy()
+    P = pts.shape[0]
+    deg = np.bincount(T.reshape(-1), minlength=P)
+    owner = {}
+    for t in range(T.shape[0]):
+        for i in range(3):
+            owner[(int(T[t, i]), int(T[t, (i + 1) % 3]))] = t
+    rng = np.random.default_rng(seed)
+    used = np.zeros(P, dtype=bool)
+    done = 0
+    for t1 in rng.permutation(T.shape[0]):
+        if done >= n_flips:
+            break
+        i = int(rng.integers(3))
+        a, b, c = int(T[t1, i]), int(T[t1, (i + 1) % 3]), int(T[t1, (i + 2) % 3])
+        t2 = owner.get((b, a))
+        if t2 is None:
+            continue
+        d = [int(v) for v in T[t2] if v != a and v != b][0]
+        if used[[a, b, c, d]].any() or deg[a] < 6 or deg[b] < 6 or deg[c] >= max_deg or deg[d] >= max_deg:
+            continue
+        ok = True
+        for tri in ((a, d, c), (d, b, c)):  # both new triangles counter-clockwise from outside
+            p0, p1, p2 = pts[tri[0]], pts[tri[1]], pts[tri[2]]
+            if np.dot(np.cross(p1 - p0, p2 - p0), p0 + p1 + p2) <= 0.0:
+                ok = False
+        if not ok:
+            continue
+        T[t1] = (a, d, c)
+        T[t2] = (d, b, c)
+        deg[a] -= 1; deg[b] -= 1; deg[c] += 1; deg[d] += 1
+        used[[a, b, c, d]] = True
+        done += 1
+    return T
+
+
 def make_mesh(n: int, n_levels: int = 60, land: str = "continents", max_edges: int = 7,
               jitter: float = 0.05, seed: int = 7, radius: float = SPHERE_RADIUS,
-              total_depth: float = 4000.0) -> Mesh:
+              total_depth: float = 4000.0, flips: int = 0, edges: bool = True) -> Mesh:
+    """``flips``: diagonal flips that give the mesh heptagons (and pentagons), see _flip_edges;
+    ``edges``: also build the edge arrays (edgesOnCell, cellsOnEdge, edgeCoord)."""
     pts, T = geodesic_triangulation(n, jitter=jitter, seed=seed)
+    T = _flip_edges(pts, T, flips, seed + 101, max_edges)
     P = pts.shape[0]
     a, b, c = pts[T[:, 0]], pts[T[:, 1]], pts[T[:, 2]]
     cc = np.cross(b - a, c - a)
@@ -223,7 +275,39 @@ def make_mesh(n: int, n_levels: int = 60, land: str = "continents", max_edges: i
     dz = total_depth * w / w.sum()
     refBottomDepth = np.cumsum(dz)
 
+    edge_kw = {}
+    if edges:
+        # one edge per unordered neighbour pair (pre-cull ids); edge k of cell c joins its
+        # vertices k and k+1 (the triangles it shares with neighbour k)
+        kk = np.arange(max_edges)[None, :]
+        valid = (kk < deg[:, None]) & (coc >= 0)
+        ca = np.broadcast_to(np.arange(P)[:, None], coc.shape)
+        lo = np.minimum(ca, coc); hi = np.maximum(ca, coc)
+        key = np.where(valid, lo * np.int64(P) + hi, -1)
+        ukeys, inv = np.unique(key[valid], return_inverse=True)
+        eid = -np.ones(coc.shape, dtype=np.int64)
+        eid[valid] = inv
+        e_lo, e_hi = ukeys // P, ukeys % P
+        e_keep = keep[e_lo] | keep[e_hi]  # MPAS culled meshes keep every edge of an ocean cell
+        new_edge = -np.ones(ukeys.size, dtype=np.int64)
+        new_edge[e_keep] = np.arange(e_keep.sum())
+        # the edge's two vertices: (c, k) and (c, k+1) of any cell that has it
+        cs, ks = np.nonzero(valid)
+        k1 = np.where(ks + 1 < deg[cs], ks + 1, 0)
+        ev = np.empty((ukeys.size, 2), dtype=np.int64)
+        ev[eid[cs, ks], 0] = voc[cs, ks]
+        ev[eid[cs, ks], 1] = voc[cs, k1]
+        mid = cc[ev[:, 0]] + cc[ev[:, 1]]
+        mid /= np.linalg.norm(mid, axis=1, keepdims=True)
+        eoc = eid[keep]
+        eoc1 = np.where(eoc >= 0, new_edge[np.maximum(eoc, 0)] + 1, 0)
+        coe = np.stack([new_cell[e_lo[e_keep]], new_cell[e_hi[e_keep]]], axis=1)
+        edge_kw = dict(nEdges=int(e_keep.sum()), edgesOnCell=eoc1.reshape(-1).astype(np.uint64),
+                       cellsOnEdge=np.where(coe >= 0, coe + 1, 0).reshape(-1).astype(np.uint64),
+                       edgeCoord=np.ascontiguousarray(mid[e_keep] * radius))
+
     return Mesh(
+        **edge_kw,
         nCells=C, nVertices=V, maxEdges=max_edges, nVertLevels=L,
         cellCoord=np.ascontiguousarray(pts[keep] * radius),
         vertexCoord=np.ascontiguousarray(cc[tri_keep] * radius),
@@ -249,12 +333,18 @@ class Snapshot:
     meridionalVelocity: np.ndarray  # [C*L]
     vertVelocityTop: np.ndarray    # [C*(L+1)]
     attributes: dict               # name -> [C*L] (map order = sorted names)
+    normalVelocity: np.ndarray = None  # [E*L] edge-normal velocity (make_snapshot(normal_velocity=True))
 
 
 def make_snapshot(mesh: Mesh, timestep: int = 0, phase: float = 0.0, u0: float = 0.5,
                   u1: float = 0.25, w0: float = 1.0e-5, land_zero: bool = True,
-                  inversions: float = 0.0, inversion_seed: int = 3, topography: str = "sigma") -> Snapshot:
+                  inversions: float = 0.0, inversion_seed: int = 3, topography: str = "sigma",
+                  normal_velocity: bool = False) -> Snapshot:
     """Solid-body flow + a travelling wave-3 perturbation, decaying with depth.
+
+    ``normal_velocity``: also the MPAS edge-normal velocity [E*L] (``normalVelocity``, the input of
+    the RBF reconstruction, MPASOSolutionTBB.cpp:131-245): the mean of the two cells' xyz velocity
+    projected on the unit vector from cellsOnEdge[0] to cellsOnEdge[1]; 0 on boundary edges.
 
     ``phase`` (radians) shifts the perturbation eastward so consecutive daily
     snapshots form a time-varying (pathline) field.
@@ -302,7 +392,23 @@ def make_snapshot(mesh: Mesh, timestep: int = 0, phase: float = 0.0, u0: float =
     wv = w0 * np.sin(2.0 * lat)[:, None] * np.sin(np.pi * zi / zi[:, -1:]) * np.cos(lon - phase)[:, None]
     temp = (2.0 + 25.0 * cl ** 2) * np.exp(-zmid / 800.0) + 1.0
     salt = 34.0 + 1.5 * np.sin(lat)[:, None] * np.exp(-zmid / 1000.0) + 0.1 * np.cos(2 * lon)[:, None]
+    nvel = None
+    if normal_velocity:
+        if mesh.edgesOnCell is None:
+            raise ValueError("normal_velocity needs a mesh built with edges=True")
+        # ENU -> xyz at the cell centres (GeoConverter::convertENUVelocityToXYZ with w = 0)
+        slon, clon, slat = np.sin(lon)[:, None], np.cos(lon)[:, None], np.sin(lat)[:, None]
+        uxyz = np.stack([-slon * u - slat * clon * v, clon * u - slat * slon * v, cl * v], axis=-1)  # [C, L, 3]
+        coe = mesh.cellsOnEdge.reshape(-1, 2).astype(np.int64) - 1
+        inner = (coe >= 0).all(axis=1)
+        a, b = coe[inner, 0], coe[inner, 1]
+        nrm = mesh.cellCoord[b] - mesh.cellCoord[a]
+        nrm /= np.linalg.norm(nrm, axis=1, keepdims=True)
+        nvel = np.zeros((mesh.nEdges, L))
+        nvel[inner] = np.einsum("elk,ek->el", 0.5 * (uxyz[a] + uxyz[b]), nrm)
+        nvel = np.ascontiguousarray(nvel.reshape(-1))
     return Snapshot(
+        normalVelocity=nvel,
         timestep=timestep,
         layerThickness=np.ascontiguousarray(thick.reshape(-1)),
         bottomDepth=np.ascontiguousarray(bot),

@@ -15,6 +15,7 @@
  *   rotate                  src/CPU/TBB/Kernel/TBBKernel.h:168-206
  *   wachspress/tri_area     src/Utils/Interpolation.hpp:95-110,137-165
  *   orc_gauss_elimination   src/Utils/Interpolation.hpp:174-217
+ *   orc_center_velocity_rbf src/CPU/TBB/MPASOSolutionTBB.cpp:131-245 + Interpolation.hpp:167-340
  *   orc_cell_center_ztop    src/Core/MPASOSolution.cpp:535-618
  *   orc_cell_to_vertex      src/CPU/TBB/MPASOSolutionTBB.cpp:9-106, 270-366
  *   orc_center_velocity_zm  src/CPU/TBB/MPASOSolutionTBB.cpp:108-129 + GeoConverter.hpp:225-247
@@ -634,30 +635,153 @@ void orc_knn(int64_t C, const double* cell_coord, int64_t n, const double* pts, 
     }
 }
 
-/* Interpolator::gauss_elimination_fixed (partial pivoting via an index
- * permutation), used by the reference's RBF reconstruction; pinned by
- * test/test_gaussian.cpp:9-27.  A is n x n row-major (modified in place). */
-void orc_gauss_elimination(double* A, double* b, int n, double* x) {
-    int pivot[64];
+/* ---------------- RBF cell-centre velocity from edge normals ---------------- */
+
+/* Interpolator::evaluate_rbf (Interpolation.hpp:169-172) */
+static double rbf_eval(double r2) { return 1.0 / sqrt(1.0 + r2); }
+
+/* Interpolator::gauss_elimination_fixed on the fixed 8 x 8 storage (Interpolation.hpp:174-217) */
+static void gauss8(double A[8][8], double b[8], int n, double x[8]) {
+    int pivot[8];
     for (int i = 0; i < n; i++) pivot[i] = i;
     for (int j = 0; j < n - 1; ++j) {
         int maxRow = j;
         for (int i = j + 1; i < n; ++i)
-            if (fabs(A[pivot[i] * n + j]) > fabs(A[pivot[maxRow] * n + j])) maxRow = i;
+            if (fabs(A[pivot[i]][j]) > fabs(A[pivot[maxRow]][j])) maxRow = i;
         int tmp = pivot[j]; pivot[j] = pivot[maxRow]; pivot[maxRow] = tmp;
         for (int i = j + 1; i < n; ++i) {
-            double factor = A[pivot[i] * n + j] / A[pivot[j] * n + j];
-            A[pivot[i] * n + j] = factor;
-            for (int k = j + 1; k < n; ++k) A[pivot[i] * n + k] -= factor * A[pivot[j] * n + k];
+            double factor = A[pivot[i]][j] / A[pivot[j]][j];
+            A[pivot[i]][j] = factor;
+            for (int k = j + 1; k < n; ++k) A[pivot[i]][k] -= factor * A[pivot[j]][k];
             b[pivot[i]] -= factor * b[pivot[j]];
         }
     }
-    x[n - 1] = b[pivot[n - 1]] / A[pivot[n - 1] * n + n - 1];
+    x[n - 1] = b[pivot[n - 1]] / A[pivot[n - 1]][n - 1];
     for (int i = n - 2; i >= 0; --i) {
         double sum = 0.0;
-        for (int j = i + 1; j < n; ++j) sum += A[pivot[i] * n + j] * x[j];
-        x[i] = (b[pivot[i]] - sum) / A[pivot[i] * n + i];
+        for (int j = i + 1; j < n; ++j) sum += A[pivot[i]][j] * x[j];
+        x[i] = (b[pivot[i]] - sum) / A[pivot[i]][i];
     }
+}
+
+/* Interpolator::mpas_rbf_interp_func_3D_plane_vec_const_dir_comp_coeffs (Interpolation.hpp:234-340) */
+static void rbf_coeffs(int n, double src[8][3], double unit[8][3], const double dst[3], double alpha,
+                       double pb[2][3], double coef[8][3]) {
+    double ps[8][2] = {{0}}, pu[8][2] = {{0}}, pd[2] = {0};
+    for (int i = 0; i < n; ++i) {
+        ps[i][0] = src[i][0] * pb[0][0] + src[i][1] * pb[0][1] + src[i][2] * pb[0][2];
+        ps[i][1] = src[i][0] * pb[1][0] + src[i][1] * pb[1][1] + src[i][2] * pb[1][2];
+        pu[i][0] = unit[i][0] * pb[0][0] + unit[i][1] * pb[0][1] + unit[i][2] * pb[0][2];
+        pu[i][1] = unit[i][0] * pb[1][0] + unit[i][1] * pb[1][1] + unit[i][2] * pb[1][2];
+    }
+    for (int d = 0; d < 2; ++d) pd[d] = dst[0] * pb[d][0] + dst[1] * pb[d][1] + dst[2] * pb[d][2];
+    double A[8][8] = {{0}}, rhs[8][2] = {{0}};
+    for (int j = 0; j < n; ++j) {
+        for (int i = j; i < n; ++i) {
+            double r2 = 0.0;
+            for (int d = 0; d < 2; ++d) { double diff = ps[i][d] - ps[j][d]; r2 += diff * diff; }
+            r2 /= (alpha * alpha);
+            double rv = rbf_eval(r2);
+            double dp = pu[i][0] * pu[j][0] + pu[i][1] * pu[j][1];
+            A[i][j] = rv * dp;
+            A[j][i] = A[i][j];
+        }
+        /* the reference computes the destination distance, then evaluates the RBF at 1.0 (:294-302) */
+        double rdst = 0.0;
+        for (int d = 0; d < 2; ++d) { double diff = pd[d] - ps[j][d]; rdst += diff * diff; }
+        rdst /= (alpha * alpha);
+        (void)rdst;
+        double rvd = rbf_eval(1.0);
+        rhs[j][0] = rvd * pu[j][0];
+        rhs[j][1] = rvd * pu[j][1];
+    }
+    double x1[8] = {0}, x2[8] = {0}, Ac[8][8], b[8];
+    for (int i = 0; i < n; ++i) for (int j = 0; j < n; ++j) Ac[i][j] = A[i][j];
+    for (int i = 0; i < n; ++i) b[i] = rhs[i][0];
+    gauss8(Ac, b, n, x1);
+    for (int i = 0; i < n; ++i) for (int j = 0; j < n; ++j) Ac[i][j] = A[i][j];
+    for (int i = 0; i < n; ++i) b[i] = rhs[i][1];
+    gauss8(Ac, b, n, x2);
+    for (int i = 0; i < n; ++i)
+        for (int d = 0; d < 3; ++d) coef[i][d] = pb[0][d] * x1[i] + pb[1][d] * x2[i];
+}
+
+/* TBBBackend::CalcCellCenterVelocity (MPASOSolutionTBB.cpp:131-245): the cell-centre xyz velocity
+ * [C*L*3] from the edge-normal velocity [E*L] by the reference's 7-point plane RBF (alpha forced to
+ * 1, pointCount = MAX_VERTEX_NUM = 7 whatever nEdgesOnCell is: absent edges enter as zero points with
+ * zero unit vectors).  Connectivity is the reference's size_t 1-based form (0 = none); every cell
+ * must have nEdgesOnCell <= 7 (the reference's arrays hold 7). */
+void orc_center_velocity_rbf(int64_t C, int L, int maxE, const uint64_t* n_edges_on_cell,
+                             const uint64_t* edges_on_cell, const uint64_t* cells_on_edge, const double* edge_coord,
+                             const double* cell_coord, const double* normal_vel, double* out) {
+    const int NV = 7;
+    const uint64_t none = UINT64_MAX;
+#ifdef _OPENMP
+#pragma omp parallel for schedule(static)
+#endif
+    for (int64_t c = 0; c < C; ++c) {
+        v3 pos = ld(cell_coord, c);
+        const uint64_t nv = n_edges_on_cell[c];
+        uint64_t eid[7];
+        for (uint64_t k = 0; k < nv && k < 7; ++k) eid[k] = edges_on_cell[c * maxE + k] - 1;
+        for (uint64_t k = nv; k < 7; ++k) eid[k] = none;
+        v3 up = dvs(pos, len(pos));
+        v3 east = cross(mk(0.0, 0.0, 1.0), up);
+        if (len(east) < 1e-6) east = cross(mk(0.0, 1.0, 0.0), up);
+        east = dvs(east, len(east));
+        v3 north = cross(up, east);
+        double pb[2][3] = {{east.x, east.y, east.z}, {north.x, north.y, north.z}};
+        double center[3] = {pos.x, pos.y, pos.z};
+        for (int k = 0; k < L; ++k) {
+            double ec[8][3] = {{0}}, uv[8][3] = {{0}}, nvel[8] = {0}, coef[8][3] = {{0}};
+            for (int s = 0; s < NV; ++s) {
+                const uint64_t e = eid[s];
+                if (e == none) continue;
+                v3 ep = ld(edge_coord, (int64_t)e);
+                ec[s][0] = ep.x; ec[s][1] = ep.y; ec[s][2] = ep.z;
+                uint64_t c0 = cells_on_edge[e * 2 + 0] - 1, c1 = cells_on_edge[e * 2 + 1] - 1;
+                uint64_t lo = c0 < c1 ? c0 : c1, hi = c0 > c1 ? c0 : c1;
+                v3 nrm;
+                double l;
+                if (hi > (uint64_t)C) {
+                    nrm = sub(ep, ld(cell_coord, (int64_t)lo));
+                    l = len(nrm);
+                    if (l == 0.0) continue;
+                    nrm = dvs(nrm, l);
+                } else {
+                    nrm = sub(ld(cell_coord, (int64_t)hi), ld(cell_coord, (int64_t)lo));
+                    l = len(nrm);
+                    if (l == 0.0) continue;
+                    nrm = dvs(nrm, l);
+                }
+                nvel[s] = normal_vel[e * (uint64_t)L + (uint64_t)k];
+                uv[s][0] = nrm.x; uv[s][1] = nrm.y; uv[s][2] = nrm.z;
+            }
+            rbf_coeffs(NV, ec, uv, center, 1.0, pb, coef);
+            double xv = 0.0, yv = 0.0, zv = 0.0;
+            for (int s = 0; s < NV; ++s) {
+                xv += coef[s][0] * nvel[s];
+                yv += coef[s][1] * nvel[s];
+                zv += coef[s][2] * nvel[s];
+            }
+            double* o = out + 3 * (c * L + k);
+            o[0] = xv; o[1] = yv; o[2] = zv;
+        }
+    }
+}
+
+/* Interpolator::gauss_elimination_fixed (partial pivoting via an index permutation) on its fixed
+ * 8 x 8 storage -- the solver of the RBF reconstruction above; pinned by test/test_gaussian.cpp:9-27
+ * (tests/golden/gauss_kat.json).  A is n x n row-major, n <= 8 (copied; not modified). */
+void orc_gauss_elimination(double* A, double* b, int n, double* x) {
+    double a8[8][8] = {{0}}, b8[8] = {0}, x8[8] = {0};
+    if (n < 1 || n > 8) return;
+    for (int i = 0; i < n; ++i) {
+        for (int j = 0; j < n; ++j) a8[i][j] = A[i * n + j];
+        b8[i] = b[i];
+    }
+    gauss8(a8, b8, n, x8);
+    for (int i = 0; i < n; ++i) x[i] = x8[i];
 }
 
 int orc_max_threads(void) {

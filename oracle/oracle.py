@@ -53,6 +53,7 @@ def lib():
         _lib.orc_center_velocity_zm.argtypes = [C.c_int64, C.c_int, P, P, P, P]
         _lib.orc_knn.argtypes = [C.c_int64, P, C.c_int64, P, P, C.c_int]
         _lib.orc_gauss_elimination.argtypes = [P, P, C.c_int, P]
+        _lib.orc_center_velocity_rbf.argtypes = [C.c_int64, C.c_int, C.c_int, P, P, P, P, P, P, P]
         _lib.orc_max_threads.restype = C.c_int
     return _lib
 
@@ -98,8 +99,25 @@ class Derived:
         return f
 
 
-def preprocess(mesh, snap) -> Derived:
-    """MOPSApp::addSol derived fields (MOPSApp.cpp:100-129) via the oracle."""
+def center_velocity_rbf(mesh, normal_velocity):
+    """TBBBackend::CalcCellCenterVelocity (MPASOSolutionTBB.cpp:131-245): cell-centre xyz velocity
+    [C*L*3] from the edge-normal velocity [E*L] (the RBF path, no live caller in the reference)."""
+    Cn, Lv = mesh.nCells, mesh.nVertLevels
+    out = np.empty(Cn * Lv * 3)
+    lib().orc_center_velocity_rbf(Cn, Lv, mesh.maxEdges,
+                                  _p(np.ascontiguousarray(mesh.nEdgesOnCell, dtype=np.uint64)),
+                                  _p(np.ascontiguousarray(mesh.edgesOnCell, dtype=np.uint64)),
+                                  _p(np.ascontiguousarray(mesh.cellsOnEdge, dtype=np.uint64)),
+                                  _p(np.ascontiguousarray(mesh.edgeCoord, dtype=np.float64)),
+                                  _p(np.ascontiguousarray(mesh.cellCoord, dtype=np.float64)),
+                                  _p(np.ascontiguousarray(normal_velocity, dtype=np.float64)), _p(out))
+    return out
+
+
+def preprocess(mesh, snap, velocity: str = "zonal") -> Derived:
+    """MOPSApp::addSol derived fields (MOPSApp.cpp:100-129) via the oracle.  ``velocity``: "zonal"
+    (CalcCellCenterVelocityByZM, the live path) or "rbf" (CalcCellCenterVelocity from
+    snap.normalVelocity, MPASOSolution::calcCellCenterVelocity)."""
     L = lib()
     Cn, V, Lv = mesh.nCells, mesh.nVertices, mesh.nVertLevels
     cc = np.ascontiguousarray(mesh.cellCoord); vc = np.ascontiguousarray(mesh.vertexCoord)
@@ -108,8 +126,11 @@ def preprocess(mesh, snap) -> Derived:
     L.orc_cell_center_ztop(Cn, Lv, _p(snap.layerThickness), _p(snap.bottomDepth), None, _p(ztc))
     ztv = np.empty(V * Lv)
     L.orc_cell_to_vertex(Cn, V, Lv, 1, 0, _p(cov), _p(cc), _p(vc), _p(ztc), _p(ztv))
-    velc = np.empty(Cn * Lv * 3)
-    L.orc_center_velocity_zm(Cn, Lv, _p(cc), _p(snap.zonalVelocity), _p(snap.meridionalVelocity), _p(velc))
+    if velocity == "rbf":
+        velc = center_velocity_rbf(mesh, snap.normalVelocity)
+    else:
+        velc = np.empty(Cn * Lv * 3)
+        L.orc_center_velocity_zm(Cn, Lv, _p(cc), _p(snap.zonalVelocity), _p(snap.meridionalVelocity), _p(velc))
     velv = np.empty(V * Lv * 3)
     L.orc_cell_to_vertex(Cn, V, Lv, 3, 0, _p(cov), _p(cc), _p(vc), _p(velc), _p(velv))
     wv = np.empty(V * (Lv + 1))

@@ -115,12 +115,17 @@ def _check_lines(got, ref, idx):
 
 
 def _check_shells(got, dead):
+    """Every line of a particle alive through the whole chain is finite and stays on its shell.
+    ``dead`` is the last pair's death steps: a particle that died in an earlier pair has zero records
+    after its death (quirk Q1) and continues from there, so lines touching the origin are excluded."""
     import torch
-    live = torch.as_tensor(~dead, device=got["points"].device)
+    r = torch.linalg.norm(got["points"], dim=-1)
+    live = torch.as_tensor(~dead, device=r.device) & (r.min(dim=1).values > 1e6)
+    assert live.float().mean().item() > 0.9
     p = got["points"][live]
     assert torch.isfinite(p).all()
-    r = torch.linalg.norm(p, dim=-1)
-    assert (r - r[:, :1]).abs().max().item() < 1e3
+    rl = r[live]
+    assert (rl - rl[:, :1]).abs().max().item() < 1e3
 
 
 def test_config4_orrs_daily_pairs(orrs, oracle_lib):

@@ -168,3 +168,24 @@ def test_config1_plumbing_on_the_oracle(oracle_lib):
         assert np.all(np.abs(rad - rad[:, :1]) < 1e3)
         dead[euler] = int((~live).sum())
     assert dead[False] > dead[True]
+
+
+def test_rbf_reconstruction_quirks(oracle_lib):
+    """The oracle's restatement of the reference's RBF reconstruction (MPASOSolutionTBB.cpp:131-245):
+    the 7-point stencil is singular for every cell with fewer than 7 edges (NaN) and finite on
+    heptagons, where -- alpha forced to 1 on a metre-scale plane, right-hand side at rbf(1) -- it
+    returns about 2.5x the cell's zonal/meridional velocity (both quirks of the reference)."""
+    from mops_amd import synth
+    m = synth.make_mesh(16, n_levels=6, flips=40)
+    s = synth.make_snapshot(m, normal_velocity=True)
+    v = oracle_lib.center_velocity_rbf(m, s.normalVelocity).reshape(m.nCells, 6, 3)
+    ne = m.nEdgesOnCell.astype(np.int64)
+    fin = np.isfinite(v).all(axis=(1, 2))
+    assert fin[ne == 7].all() and not fin[ne < 7].any()
+    zm = oracle_lib.preprocess(m, s).cell_vel.reshape(m.nCells, 6, 3)
+    h = ne == 7
+    ratio = np.median(np.linalg.norm(v[h], axis=-1) / np.linalg.norm(zm[h], axis=-1))
+    assert 2.0 < ratio < 3.0
+    # the derivation chain takes the RBF velocity when asked
+    d = oracle_lib.preprocess(m, s, velocity="rbf")
+    assert np.array_equal(d.cell_vel, v.reshape(-1), equal_nan=True)
