@@ -188,11 +188,22 @@ __device__ __forceinline__ double sqrt_core(double x) {
 #ifndef MOPS_FAST_SQRT
 #define MOPS_FAST_SQRT 1
 #endif
+#ifndef MOPS_SQRT_ONESIDED
+#define MOPS_SQRT_ONESIDED 0
+#endif
 __device__ __forceinline__ double xsqrt(double x) {
+#if MOPS_FAST_SQRT && MOPS_SQRT_ONESIDED
+    // the core result always, the library's only for the rare out-of-range x: a one-sided branch
+    // (fewer exec-mask instructions than if/else)
+    double r = sqrt_core(x);
+    if (__builtin_expect(!(x >= 0x1p-767 && x < __builtin_huge_val()), 0)) r = sqrt(x);
+    return r;
+#else
 #if MOPS_FAST_SQRT
     if (__builtin_expect(x >= 0x1p-767 && x < __builtin_huge_val(), 1)) return sqrt_core(x);
 #endif
     return sqrt(x);
+#endif
 }
 #endif
 
