@@ -93,6 +93,8 @@ def parse():
     p.add_argument("--compact", choices=["auto", "on", "off"], default="auto",
                    help="config 2: re-sort each particle part with its dead particles last between step chunks "
                         "(ParticleSet.compact); auto = on for RK4 (quirk Q1 kills half the particles in a day)")
+    p.add_argument("--compact-priority", action="store_true",
+                   help="run the compaction re-sorts on high-priority streams (experiment)")
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--cpu-seconds", type=float, default=12.0, help="target CPU-baseline sample length")
     return p.parse_args()
@@ -389,7 +391,8 @@ def main():
                 nch = max(1, round(args.chunks * (s1 - s0) / n_steps))
                 ps_.advance_pipelined(dfield, dback, s0, s1, part_streams, nch,
                                      timing=dispatch_ms if timed else None,
-                                     compact=compact or (pset is not None and args.compact != "off"))
+                                     compact=compact or (pset is not None and args.compact != "off"),
+                                     compact_priority=args.compact_priority)
                 for st in part_streams:
                     j = torch.cuda.Event(); j.record(st); compute.wait_event(j)
                 e1.record(compute)

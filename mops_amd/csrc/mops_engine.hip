@@ -84,6 +84,7 @@ struct mops_mesh {
     double4* d_cxyz = nullptr;   // [C] (x,y,z,0)
     double4* d_vxyz = nullptr;   // [V]
     int* d_cov = nullptr;        // [V][3] cellsOnVertex 0-based, -1 = missing (boundary)
+    double4* d_bary = nullptr;   // [V] barycentric weights in the cellsOnVertex centres (vertex_bary_kernel)
     // seed-location bucket index
     double bucket_h = 0.0, bucket_origin = 0.0;
     int origin_cell = -1;  // exact nearest centre to (0,0,0) (locate_kernel's tie rule)
@@ -189,7 +190,7 @@ __device__ __forceinline__ double sqrt_core(double x) {
 #define MOPS_FAST_SQRT 1
 #endif
 #ifndef MOPS_SQRT_ONESIDED
-#define MOPS_SQRT_ONESIDED 0
+#define MOPS_SQRT_ONESIDED 1  // measured: streamline Euler segment 27.0 -> 26.0 ms, RK4 86.5 -> 85.2 ms
 #endif
 __device__ __forceinline__ double xsqrt(double x) {
 #if MOPS_FAST_SQRT && MOPS_SQRT_ONESIDED
@@ -290,8 +291,16 @@ __device__ __forceinline__ double len3(double x, double y, double z) { return xs
 #endif
 __device__ __forceinline__ void xdiv_norm3(double a0, double a1, double a2, double b, double& q0, double& q1,
                                            double& q2) {
+#ifndef MOPS_DIV3_ONESIDED
+#define MOPS_DIV3_ONESIDED 0
+#endif
 #if MOPS_FAST_DIV3 && !defined(MOPS_ABL_DIV)
-    if (__builtin_expect(b <= 0x1p300 && fabs(a0) >= 0x1p-700 && fabs(a1) >= 0x1p-700 && fabs(a2) >= 0x1p-700, 1)) {
+    const bool fast = b <= 0x1p300 && fabs(a0) >= 0x1p-700 && fabs(a1) >= 0x1p-700 && fabs(a2) >= 0x1p-700;
+#if MOPS_DIV3_ONESIDED
+    if (true) {  // the fast quotients always; `/` replaces them for the rare operands outside the range
+#else
+    if (__builtin_expect(fast, 1)) {
+#endif
         double r = __builtin_amdgcn_rcp(b);
         double e = __builtin_fma(-b, r, 1.0);
         r = __builtin_fma(r, e, r);
@@ -303,6 +312,9 @@ __device__ __forceinline__ void xdiv_norm3(double a0, double a1, double a2, doub
         q1 = __builtin_fma(__builtin_fma(-b, q, a1), r, q);
         q = a2 * r;
         q2 = __builtin_fma(__builtin_fma(-b, q, a2), r, q);
+#if MOPS_DIV3_ONESIDED
+        if (__builtin_expect(!fast, 0)) { q0 = xdiv(a0, b); q1 = xdiv(a1, b); q2 = xdiv(a2, b); }
+#endif
         return;
     }
 #endif
@@ -337,6 +349,17 @@ __device__ __forceinline__ void rotate(unsigned salt, double px, double py, doub
 #ifndef MOPS_FAST_TRIG
 #define MOPS_FAST_TRIG 1
 #endif
+#ifndef MOPS_TRIG_ONESIDED
+#define MOPS_TRIG_ONESIDED 0
+#endif
+#if MOPS_TRIG_ONESIDED
+    sincos_small(th, s, c, salt);  // always; the library's values replace it for the rare |th| >= 0.78
+    if (!MOPS_FAST_TRIG || __builtin_expect(!(fabs(th) < 0.78), 0)) {
+        const double2 sc = sincos_lib(th);
+        s = sc.x;
+        c = sc.y;
+    }
+#else
     if (MOPS_FAST_TRIG && __builtin_expect(fabs(th) < 0.78, 1)) {
         sincos_small(th, s, c, salt);
     } else {
@@ -344,6 +367,7 @@ __device__ __forceinline__ void rotate(unsigned salt, double px, double py, doub
         s = sc.x;
         c = sc.y;
     }
+#endif
 #endif
     const double al = len3(ax, ay, az);
     if (al <= 1e-12) { rx = px; ry = py; rz = pz; return; }
@@ -1524,23 +1548,45 @@ __global__ void __launch_bounds__(256) assemble_kernel(int64_t n, int64_t K, con
 // derived-field preprocessing (once per snapshot)
 // ===========================================================================
 
-// MPASOSolution::calcCellCenterZtop (MPASOSolution.cpp:535-618)
-__global__ void cell_ztop_kernel(int64_t C, int L, const double* thick, const double* bottom, const double* ssh,
-                                 double* ztop) {
-    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= C) return;
-    if (bottom) {
-        double z = -bottom[i];
-        for (int k = L - 1; k >= 0; --k) { z += thick[L * i + k]; ztop[i * L + k] = z * 1.0; }
-    } else if (ssh) {
-        double z = ssh[i];
-        ztop[i * L] = z * 1.0;
-        for (int j = 1; j < L; ++j) { z -= thick[L * i + j - 1]; ztop[i * L + j] = z * 1.0; }
-    } else {
-        double prev = 0.0;
-        ztop[i * L] = 0.0;
-        for (int j = 1; j < L; ++j) { prev = prev - thick[L * i + j - 1]; ztop[i * L + j] = prev * 1.0; }
+// MPASOSolution::calcCellCenterZtop (MPASOSolution.cpp:535-618): zTop from layerThickness and
+// bottomDepth (bottom up), or from the surface height (top down), or from 0; each row's
+// recurrence in the reference's order, with the block's rows staged through LDS: kZtCells consecutive cells are
+// one contiguous [kZtCells][L] slab of thick (and of ztop), so it is read and written with
+// coalesced wave-wide accesses; one thread per cell runs its row's recurrence in LDS, in the
+// reference's order (a per-cell thread streaming its own row made every wave access 64 rows L
+// doubles apart: 0.6 TB/s on an oRRS18to6-class snapshot).
+constexpr int kZtCells = 64;
+__global__ void __launch_bounds__(256) cell_ztop_tiled_kernel(int64_t C, int L, const double* __restrict__ thick,
+                                                              const double* __restrict__ bottom,
+                                                              const double* __restrict__ ssh,
+                                                              double* __restrict__ ztop) {
+    extern __shared__ double zt_tile[];  // [kZtCells * L]
+    const int64_t c0 = (int64_t)blockIdx.x * kZtCells;
+    const int nc = (int)((C - c0) < kZtCells ? (C - c0) : kZtCells);
+    const int64_t base = c0 * L;
+    const int n = nc * L;
+    for (int i = threadIdx.x; i < n; i += blockDim.x) zt_tile[i] = thick[base + i];
+    __syncthreads();
+    if ((int)threadIdx.x < nc) {
+        double* row = zt_tile + threadIdx.x * L;
+        const int64_t i = c0 + threadIdx.x;
+        if (bottom) {
+            double z = -bottom[i];
+            for (int k = L - 1; k >= 0; --k) { z += row[k]; row[k] = z * 1.0; }
+        } else if (ssh) {
+            double z = ssh[i];
+            double tp = row[0];  // thick[j-1] for j = 1, read before row[0] is overwritten
+            row[0] = z * 1.0;
+            for (int j = 1; j < L; ++j) { const double t = row[j]; z -= tp; row[j] = z * 1.0; tp = t; }
+        } else {
+            double prev = 0.0;
+            double tp = row[0];
+            row[0] = 0.0;
+            for (int j = 1; j < L; ++j) { const double t = row[j]; prev = prev - tp; row[j] = prev * 1.0; tp = t; }
+        }
     }
+    __syncthreads();
+    for (int i = threadIdx.x; i < n; i += blockDim.x) ztop[base + i] = zt_tile[i];
 }
 
 // CalcCellCenterVelocityByZM + GeoConverter::convertENUVelocityToXYZ (Uup = 0)
@@ -1714,18 +1760,17 @@ __global__ void rbf_apply_kernel(int64_t C, int L, const double* __restrict__ co
 }
 
 // CalcCellVertexZtop / CenterToVertex / VertexVelocity / VertexVertVelocity
-// (MPASOSolutionTBB.cpp:9-106, 270-366): barycentric of the 3 cellsOnVertex.
-template <int DIM>
-__global__ void cell_to_vertex_kernel(int64_t V, int Lt, const int* cov, const double4* cxyz, const double4* vxyz,
-                                      const double* src, double* dst, int clamp_neg) {
-    const int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (idx >= V * Lt) return;
-    const int64_t vid = idx / Lt;
-    const int k = (int)(idx % Lt);
+// (MPASOSolutionTBB.cpp:9-106, 270-366): barycentric of the 3 cellsOnVertex.  The weights of each
+// vertex in its three cellsOnVertex centres are computed once per mesh (the reference recomputes
+// them per (vertex, level); same operations, so bit-identical): {u, v, w, 1}, or {0, 0, 0, 0}
+// for a boundary vertex (a missing cell, quirk Q10); cell_to_vertex_bary_kernel then applies them
+// to every level.
+__global__ void vertex_bary_kernel(int64_t V, const int* __restrict__ cov, const double4* __restrict__ cxyz,
+                                   const double4* __restrict__ vxyz, double4* __restrict__ bary) {
+    const int64_t vid = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (vid >= V) return;
     const int c0 = cov[3 * vid], c1 = cov[3 * vid + 1], c2 = cov[3 * vid + 2];
-    double out[DIM];
-#pragma unroll
-    for (int d = 0; d < DIM; ++d) out[d] = 0.0;
+    double4 b = make_double4(0.0, 0.0, 0.0, 0.0);
     if (c0 >= 0 && c1 >= 0 && c2 >= 0) {
         const double4 p = vxyz[vid], A = cxyz[c0], B = cxyz[c1], Cc = cxyz[c2];
         const double v0x = B.x - A.x, v0y = B.y - A.y, v0z = B.z - A.z;
@@ -1740,12 +1785,31 @@ __global__ void cell_to_vertex_kernel(int64_t V, int Lt, const int* cov, const d
         const double v = (d11 * d20 - d01 * d21) / den;
         const double w = (d00 * d21 - d01 * d20) / den;
         const double u = 1.0 - v - w;
+        b = make_double4(u, v, w, 1.0);
+    }
+    bary[vid] = b;
+}
+
+template <int DIM>
+__global__ void cell_to_vertex_bary_kernel(int64_t V, int Lt, const int* __restrict__ cov,
+                                           const double4* __restrict__ bary, const double* __restrict__ src,
+                                           double* __restrict__ dst, int clamp_neg) {
+    const int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (idx >= V * Lt) return;
+    const int64_t vid = idx / Lt;
+    const int k = (int)(idx - vid * Lt);
+    const double4 b = bary[vid];
+    double out[DIM];
+#pragma unroll
+    for (int d = 0; d < DIM; ++d) out[d] = 0.0;
+    if (b.w != 0.0) {
+        const int c0 = cov[3 * vid], c1 = cov[3 * vid + 1], c2 = cov[3 * vid + 2];
 #pragma unroll
         for (int d = 0; d < DIM; ++d) {
             const double a0 = src[((int64_t)c0 * Lt + k) * DIM + d];
             const double a1 = src[((int64_t)c1 * Lt + k) * DIM + d];
             const double a2 = src[((int64_t)c2 * Lt + k) * DIM + d];
-            double o = u * a0 + v * a1 + w * a2;
+            double o = b.x * a0 + b.y * a1 + b.z * a2;
             if (clamp_neg && o < 0.0) o = 0.0;
             out[d] = o;
         }
@@ -2084,7 +2148,13 @@ __global__ void pair_record_kernel(int64_t V, int L, const double* __restrict__ 
 // tile of kRecTV vertices x (kRecTK + 1) levels through LDS (reads run along each vertex's
 // column) and writes kRecTK rows of kRecTV consecutive records (contiguous 5 KB per row), so
 // both sides are coalesced.  Same values and chunk layout as pair_record_kernel.
-constexpr int kRecTV = 64, kRecTK = 16;
+#ifndef MOPS_REC_TV
+#define MOPS_REC_TV 64
+#endif
+#ifndef MOPS_REC_TK
+#define MOPS_REC_TK 16
+#endif
+constexpr int kRecTV = MOPS_REC_TV, kRecTK = MOPS_REC_TK;
 __global__ void __launch_bounds__(256) pair_record_tiled_kernel(int64_t V, int L, const double* __restrict__ zt,
                                                                 const double* __restrict__ vel,
                                                                 const double* __restrict__ w,
@@ -2205,6 +2275,7 @@ mops_status upload(const T* h, size_t count, T** d, int64_t* acc, hipStream_t s)
 void free_mesh(mops_mesh* m) {
     if (!m) return;
     (void)hipFree(m->d_cellrec); (void)hipFree(m->d_cxyz); (void)hipFree(m->d_vxyz); (void)hipFree(m->d_cov);
+    (void)hipFree(m->d_bary);
     (void)hipFree(m->d_bkeys); (void)hipFree(m->d_bcells); (void)hipFree(m->d_hkeys); (void)hipFree(m->d_hval); (void)hipFree(m->d_cell_key); (void)hipFree(m->d_cellB); (void)hipFree(m->d_rloc2); (void)hipFree(m->d_ring);
     (void)hipFree(m->d_scratch);
     (void)hipFree(m->d_eoc); (void)hipFree(m->d_coe); (void)hipFree(m->d_exyz); (void)hipFree(m->d_rbf_coef);
@@ -2383,6 +2454,8 @@ mops_status mops_mesh_create(const mops_mesh_desc* desc, void* stream, mops_mesh
             } else cov[i] = (int)(x - 1);
         }
         if ((st = upload(cov.data(), cov.size(), &m->d_cov, &acc, s)) != MOPS_OK) { free_mesh(m); return st; }
+        if ((st = dmalloc(&m->d_bary, (size_t)V, &acc)) != MOPS_OK) { free_mesh(m); return st; }
+        vertex_bary_kernel<<<grid_for(V), kBlock, 0, s>>>(V, m->d_cov, m->d_cxyz, m->d_vxyz, m->d_bary);
     }
     // ---- bucket index for seed location ----
     double rmax = 0.0, rsum = 0.0;
@@ -2630,21 +2703,19 @@ static mops_status field_derive(const mops_mesh* mesh, mops_field* f, const mops
     if (!f->d_zt) MOPS_TRY(dmalloc(&f->d_zt, (size_t)(V * L), &f->bytes));
     if (!f->d_vel) MOPS_TRY(dmalloc(&f->d_vel, (size_t)(V * L * 3), &f->bytes));
     if (!f->d_w) MOPS_TRY(dmalloc(&f->d_w, (size_t)(V * (L + 1)), &f->bytes));
-    cell_ztop_kernel<<<grid_for(C), kBlock, 0, s>>>(C, L, d->h_layer_thickness, bot, ssh, ztc);
-    cell_to_vertex_kernel<1><<<grid_for(V * L), kBlock, 0, s>>>(V, L, mesh->d_cov, mesh->d_cxyz, mesh->d_vxyz, ztc,
-                                                               f->d_zt, 0);
+    cell_ztop_tiled_kernel<<<(unsigned)((C + kZtCells - 1) / kZtCells), 256, (size_t)kZtCells * L * sizeof(double), s>>>(
+        C, L, d->h_layer_thickness, bot, ssh, ztc);
+    cell_to_vertex_bary_kernel<1><<<grid_for(V * L), kBlock, 0, s>>>(V, L, mesh->d_cov, mesh->d_bary, ztc, f->d_zt, 0);
     if (d->h_zonal_velocity && d->h_meridional_velocity) {  // the live path (MOPSApp.cpp:113)
         center_vel_zm_kernel<<<grid_for(C * L), kBlock, 0, s>>>(C, L, mesh->d_cxyz, d->h_zonal_velocity,
                                                                 d->h_meridional_velocity, velc);
     } else {  // edge normals only: the RBF reconstruction (MPASOSolution::calcCellCenterVelocity)
         MOPS_TRY(mops_cell_center_velocity_rbf(mesh, d->h_normal_velocity, velc, s));
     }
-    cell_to_vertex_kernel<3><<<grid_for(V * L), kBlock, 0, s>>>(V, L, mesh->d_cov, mesh->d_cxyz, mesh->d_vxyz, velc,
-                                                               f->d_vel, 0);
+    cell_to_vertex_bary_kernel<3><<<grid_for(V * L), kBlock, 0, s>>>(V, L, mesh->d_cov, mesh->d_bary, velc, f->d_vel, 0);
     if (d->h_vert_velocity_top) {
-        cell_to_vertex_kernel<1><<<grid_for(V * (L + 1)), kBlock, 0, s>>>(V, L + 1, mesh->d_cov, mesh->d_cxyz,
-                                                                         mesh->d_vxyz, d->h_vert_velocity_top,
-                                                                         f->d_w, 0);
+        cell_to_vertex_bary_kernel<1><<<grid_for(V * (L + 1)), kBlock, 0, s>>>(V, L + 1, mesh->d_cov, mesh->d_bary,
+                                                                              d->h_vert_velocity_top, f->d_w, 0);
     } else {
         HIP_TRY(hipMemsetAsync(f->d_w, 0, (size_t)(V * (L + 1)) * sizeof(double), s));
     }
@@ -2714,8 +2785,8 @@ mops_status mops_cell_to_vertex_attr(const mops_mesh* mesh, const double* d_cell
     if (!mesh || !d_cell_attr || !d_vertex_attr || !mesh->d_cov)
         return fail(MOPS_ERR_INVALID, "mops_cell_to_vertex_attr: null argument");
     hipStream_t s = (hipStream_t)stream;
-    cell_to_vertex_kernel<1><<<grid_for(mesh->V * mesh->L), kBlock, 0, s>>>(
-        mesh->V, mesh->L, mesh->d_cov, mesh->d_cxyz, mesh->d_vxyz, d_cell_attr, d_vertex_attr, 1);
+    cell_to_vertex_bary_kernel<1><<<grid_for(mesh->V * mesh->L), kBlock, 0, s>>>(
+        mesh->V, mesh->L, mesh->d_cov, mesh->d_bary, d_cell_attr, d_vertex_attr, 1);
     HIP_TRY(hipGetLastError());
     return MOPS_OK;
 }

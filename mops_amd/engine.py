@@ -409,7 +409,7 @@ class ParticleSet:
                            self.cell.data_ptr() + e4 * lo, self.death.data_ptr() + e4 * lo, None)
 
     def advance_pipelined(self, front: DeviceField, back: DeviceField | None, step_begin: int, step_end: int,
-                          streams, chunks: int, timing=None, compact: bool = False):
+                          streams, chunks: int, timing=None, compact: bool = False, compact_priority: bool = False):
         """``advance`` split into len(streams) contiguous particle parts (whole waves), each on its own
         stream, and ``chunks`` step ranges per part, enqueued chunk-major.
 
@@ -433,10 +433,9 @@ class ParticleSet:
         tb = [int(step_begin) + span * k // chunks for k in range(chunks + 1)]
         period = self.record_period(pathline=back is not None)
         lib = L.load()
-        if compact and chunks > 1:
-            # the re-sort runs on a high-priority stream per part: its short kernels would otherwise
-            # queue behind the other parts' trajectory waves for the CUs they free one by one
-            # (measured: the key kernel then took 5 ms instead of microseconds)
+        if compact and chunks > 1 and compact_priority:
+            # optionally the re-sort runs on a high-priority stream per part: its short kernels otherwise
+            # queue behind the other parts' trajectory waves (measured: the key kernel then waits ~5 ms)
             dev = self.seeds.device
             if getattr(self, "_hp_streams", None) is None or len(self._hp_streams) < nparts:
                 prio = torch.cuda.Stream.priority_range()[1]  # the numerically lowest = highest priority
@@ -449,10 +448,14 @@ class ParticleSet:
                 st = streams[k]
                 if compact and t > 0:
                     # slots written so far: slot 0 (step-0 pre-writes) .. the last completed record
-                    hp = self._hp_streams[k]
-                    hp.wait_stream(st)
-                    self.compact(lo, hi, hp, records_written=min(self.K, tb[t] // period + 1) if period else 1)
-                    st.wait_stream(hp)
+                    nrec = min(self.K, tb[t] // period + 1) if period else 1
+                    if compact_priority:
+                        hp = self._hp_streams[k]
+                        hp.wait_stream(st)
+                        self.compact(lo, hi, hp, records_written=nrec)
+                        st.wait_stream(hp)
+                    else:
+                        self.compact(lo, hi, st, records_written=nrec)
                 if timing is not None:
                     e0 = torch.cuda.Event(enable_timing=True); e1 = torch.cuda.Event(enable_timing=True)
                     e0.record(st)
