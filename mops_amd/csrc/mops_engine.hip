@@ -2315,6 +2315,43 @@ void launch_traj(const TrajArgs& a, bool path, bool euler, hipStream_t s) {
     }
 }
 
+// The trajectory kernel's exact fast sqrt / sin / cos / a/|a| restate the device library's and the
+// compiler's own expansions (dev::sqrt_core, sincos_small, xdiv_norm3).  A toolchain whose
+// expansions changed would break the bit parity silently, so every mesh creation first checks
+// them against the library on fixed arguments (the full sweep is mops_selftest_math's test).
+static mops_status check_fast_math(hipStream_t s) {
+    constexpr int n = 512;  // arguments per op (op 2: n vectors of 3)
+    std::vector<double> x(3 * n), out(6 * n);
+    double* d = nullptr;  // [3n inputs | 6n outputs]
+    HIP_TRY(hipMalloc(&d, 9 * n * sizeof(double)));
+    mops_status st = MOPS_OK;
+    for (int op = 0; op < 3 && st == MOPS_OK; ++op) {
+        const int nin = (op == 2) ? 3 * n : n, width = (op == 0) ? 2 : (op == 1 ? 4 : 2);  // outputs per input
+        for (int i = 0; i < nin; ++i) {
+            const double t = (i + 0.5) / nin;
+            if (op == 0) x[i] = std::ldexp(1.0 + t, -760 + (int)(t * 1700.0));   // sqrt over [2^-760, 2^940)
+            else if (op == 1) x[i] = 0.779 * std::sin(37.0 * t + 0.3);            // |x| < 0.78
+            else x[i] = std::ldexp(std::cos(91.0 * t), (int)(t * 40.0) - 20);    // components for a/|a|
+        }
+        const int nout = nin * width;  // op 2: 6 per vector = 2 per component
+        hipError_t e = hipMemcpyAsync(d, x.data(), nin * sizeof(double), hipMemcpyHostToDevice, s);
+        if (e == hipSuccess) selftest_math_kernel<<<grid_for(n), kBlock, 0, s>>>(n, d, d + 3 * n, op);
+        if (e == hipSuccess) e = hipGetLastError();
+        if (e == hipSuccess) e = hipMemcpyAsync(out.data(), d + 3 * n, nout * sizeof(double), hipMemcpyDeviceToHost, s);
+        if (e == hipSuccess) e = hipStreamSynchronize(s);
+        if (e != hipSuccess) { st = fail(MOPS_ERR_HIP, std::string("fast-math check: ") + hipGetErrorString(e)); break; }
+        // op 0: {fast, lib} per x; op 1: {fast s, lib s, fast c, lib c}; op 2: {3 fast, 3 lib} per vector
+        for (int i = 0; i < nout / 2 && st == MOPS_OK; ++i) {
+            const int a = (op == 2) ? (i / 3) * 6 + i % 3 : 2 * i, b = (op == 2) ? a + 3 : a + 1;
+            if (std::memcmp(&out[a], &out[b], sizeof(double)) != 0)
+                st = fail(MOPS_ERR_UNSUPPORTED, "the engine's exact fast-math helpers differ from the device library "
+                                                "on this toolchain (bit parity would be lost)");
+        }
+    }
+    (void)hipFree(d);
+    return st;
+}
+
 extern "C" {
 
 const char* mops_last_error(void) { return g_last_error.c_str(); }
@@ -2519,6 +2556,7 @@ mops_status mops_mesh_create(const mops_mesh_desc* desc, void* stream, mops_mesh
     e = hipGetLastError();
     if (e == hipSuccess) e = hipStreamSynchronize(s);
     if (e != hipSuccess) { free_mesh(m); return fail(MOPS_ERR_HIP, std::string("cell keys: ") + hipGetErrorString(e)); }
+    if ((st = check_fast_math(s)) != MOPS_OK) { free_mesh(m); return st; }
     m->bytes = acc;
     *out = m;
     return MOPS_OK;

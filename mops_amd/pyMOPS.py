@@ -370,13 +370,22 @@ def MOPS_End():
                                   cellsOnVertex=g.ints[G.kCellsOnVertex], cellCoord=g.vec3[G.kCellCoord],
                                   vertexCoord=g.vec3[G.kVertexCoord])
         A = AttributeType
+        # a solution with the edge-normal velocity only (kNormalVelocity) takes the RBF reconstruction
+        # (MPASOSolution::calcCellCenterVelocity), which needs the grid's edges on the device
+        rbf = {sid: (s.doubles.get(A.kZonalVelocity) is None or s.doubles.get(A.kMeridionalVelocity) is None)
+               and s.doubles.get(A.kNormalVelocity) is not None for sid, s in _app.sols.items()}
+        if any(rbf.values()):
+            _app.mesh.set_edges(len(g.vec3[G.kEdgeCoord]), g.ints[G.kEdgesOnCell], g.ints[G.kCellsOnEdge],
+                                g.vec3[G.kEdgeCoord])
         for sid, s in sorted(_app.sols.items()):
             snap = types.SimpleNamespace(
                 timestep=s.mTimesteps, layerThickness=s.doubles.get(A.kLayerThickness),
                 bottomDepth=s.doubles.get(A.kBottomDepth), surfaceHeight=s.cellSurfaceHeight,
                 zonalVelocity=s.doubles.get(A.kZonalVelocity),
-                meridionalVelocity=s.doubles.get(A.kMeridionalVelocity), vertVelocityTop=s.cellVertVelocity_vec)
-            _app.fields[sid] = _E.DeviceField.from_snapshot(_app.mesh, snap)
+                meridionalVelocity=s.doubles.get(A.kMeridionalVelocity), vertVelocityTop=s.cellVertVelocity_vec,
+                normalVelocity=s.doubles.get(A.kNormalVelocity))
+            _app.fields[sid] = _E.DeviceField.from_snapshot(_app.mesh, snap,
+                                                            velocity="rbf" if rbf[sid] else "zonal")
         if _app.fields:
             _app.front = _app.fields[min(_app.fields)]
 
