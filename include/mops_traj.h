@@ -95,6 +95,9 @@ typedef struct {
     const int32_t* d_order;              /* optional processing order (slot -> particle index),
                                             from mops_order_particles; NULL = identity.  Only
                                             affects speed, never results. */
+    const int32_t* d_n_live;             /* optional device count: only slots [0, *d_n_live) hold
+                                            live particles (after mops_order_particles_live); the
+                                            launch spreads just those over the XCDs.  NULL = all n. */
 } mops_particles;
 
 const char* mops_last_error(void);
@@ -207,14 +210,14 @@ mops_status mops_order_particles(const mops_mesh* mesh, int64_t n, const int32_t
  * parallel_for keeps visiting particles whose lambda has returned,
  * MPASOVisualizerKernels.cpp:944-957, quirk Q1).  As mops_order_particles,
  * but particles with d_death[i] >= 0 (d_death may be NULL) sort after every
- * live one, so live particles fill whole waves and all-dead waves exit at
- * their first instruction.  Re-entrant: the caller passes device scratch of
+ * live one, so live particles fill whole waves; d_n_live (device, may be
+ * NULL) receives their count, for mops_particles::d_n_live.  Re-entrant: the caller passes device scratch of
  * at least mops_order_scratch_bytes(n) bytes, so several particle parts can
  * be re-sorted concurrently on their own streams. */
 int64_t mops_order_scratch_bytes(int64_t n);
 mops_status mops_order_particles_live(const mops_mesh* mesh, int64_t n, const int32_t* d_cell,
-                                      const int32_t* d_death, int32_t* d_order, void* d_scratch,
-                                      int64_t scratch_bytes, void* stream);
+                                      const int32_t* d_death, int32_t* d_order, int32_t* d_n_live,
+                                      void* d_scratch, int64_t scratch_bytes, void* stream);
 
 /* ---- trajectory hot path (device-resident) ----------------------------- */
 

@@ -56,7 +56,7 @@ class TrajCfg(C.Structure):
 class Particles(C.Structure):
     _fields_ = [("n", C.c_int64), ("d_x", C.c_void_p), ("d_y", C.c_void_p), ("d_z", C.c_void_p),
                 ("d_depth", C.c_void_p), ("d_cell", C.c_void_p), ("d_death_step", C.c_void_p),
-                ("d_order", C.c_void_p)]
+                ("d_order", C.c_void_p), ("d_n_live", C.c_void_p)]
 
 
 class MopsError(RuntimeError):
@@ -138,7 +138,7 @@ def load(path: str | None = None):
     lib.mops_remove_nan_lines.argtypes = [I64, I64, P, P, P, P, P, P]; lib.mops_remove_nan_lines.restype = st
     lib.mops_remove_nan_ragged.argtypes = [I64, P, P, P, P, P, P, P]; lib.mops_remove_nan_ragged.restype = st
     lib.mops_order_scratch_bytes.argtypes = [I64]; lib.mops_order_scratch_bytes.restype = I64
-    lib.mops_order_particles_live.argtypes = [P, I64, P, P, P, P, I64, P]
+    lib.mops_order_particles_live.argtypes = [P, I64, P, P, P, P, P, I64, P]
     lib.mops_order_particles_live.restype = st
     lib.mops_run_trajectories.argtypes = [P, P, P, P, I64, P, P, C.c_float, P, P, P, P, P, P, P, P, P, P]
     lib.mops_run_trajectories.restype = st

@@ -1156,6 +1156,7 @@ struct TrajArgs {
     const uint32_t* __restrict__ mono0;
     const uint32_t* __restrict__ mono1;
     const int* __restrict__ order;  // slot -> particle (NULL = identity)
+    const int* __restrict__ n_live;  // device count of leading live slots (compaction), NULL = all n
     const double* __restrict__ cellB;  // per-cell Wachspress B_i
     double* px; double* py; double* pz;
     float* depth;
@@ -1238,10 +1239,22 @@ template <int MAXV, bool PATH, bool EULER>
 __global__ void __launch_bounds__(kTrajBlock, (TrajWaves<MAXV, PATH, EULER>::value)) traj_kernel(TrajArgs a) {
     // XCD-aware mapping: blocks b, b+8, ... share an XCD (L2); give each XCD a
     // contiguous range of the locality-ordered particles (bijective remap)
-    const unsigned nblk = gridDim.x, b = blockIdx.x, xcd = b % 8u, q = nblk / 8u, r = nblk % 8u;
+    // After a compaction only the first *n_live slots hold live particles: the remap then spreads
+    // just those blocks over the 8 XCDs (blocks beyond them exit at once), instead of handing the
+    // dead tail's blocks -- a contiguous range -- to whole XCDs that would sit idle
+    unsigned nblk = gridDim.x;
+    int64_t n = a.n;
+    if (a.n_live) {
+        const int64_t nl = *a.n_live;
+        n = nl < n ? nl : n;
+        nblk = (unsigned)((n + blockDim.x - 1) / blockDim.x);
+    }
+    const unsigned b = blockIdx.x;
+    if (b >= nblk) return;
+    const unsigned xcd = b % 8u, q = nblk / 8u, r = nblk % 8u;
     const unsigned blk = (xcd < r ? xcd * (q + 1u) : r * (q + 1u) + (xcd - r) * q) + b / 8u;
     const int64_t slot = (int64_t)blk * blockDim.x + threadIdx.x;
-    if (slot >= a.n) return;
+    if (slot >= n) return;
 #if defined(MOPS_WAVE_STAMPS)
     unsigned long long* stamp = dev::stamp_slot();
     if (stamp) {
@@ -2149,7 +2162,7 @@ __global__ void pair_record_kernel(int64_t V, int L, const double* __restrict__ 
 // column) and writes kRecTK rows of kRecTV consecutive records (contiguous 5 KB per row), so
 // both sides are coalesced.  Same values and chunk layout as pair_record_kernel.
 #ifndef MOPS_REC_TV
-#define MOPS_REC_TV 64
+#define MOPS_REC_TV 32  // 32 x 16 tiles: 16.4 vs 17.6 ms per oRRS18to6 snapshot (64 x 16), profiles/r03
 #endif
 #ifndef MOPS_REC_TK
 #define MOPS_REC_TK 16
@@ -2219,13 +2232,20 @@ __global__ void cell_key_kernel(int64_t C, const double4* cxyz, uint64_t* key) {
 // Morton key of each particle's cell; a dead particle (death >= 0, when given) or one without a
 // cell sorts last (~0), so live particles fill whole waves and all-dead waves exit at once
 __global__ void particle_key_kernel(int64_t n, int64_t C, const int* cell, const int* death,
-                                    const uint64_t* cell_key, uint64_t* key, int* idx) {
+                                    const uint64_t* cell_key, uint64_t* key, int* idx, int* n_live) {
     const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= n) return;
-    const int c = cell[i];
-    const bool live = !death || death[i] < 0;
-    key[i] = (live && c >= 0 && c < C) ? cell_key[c] : ~0ULL;
-    idx[i] = (int)i;
+    bool sorts_first = false;
+    if (i < n) {
+        const int c = cell[i];
+        const bool live = !death || death[i] < 0;
+        sorts_first = live && c >= 0 && c < C;
+        key[i] = sorts_first ? cell_key[c] : ~0ULL;
+        idx[i] = (int)i;
+    }
+    if (n_live) {  // one atomic per wave: the particles that sort before the ~0 keys
+        const unsigned long long m = __ballot(sorts_first);
+        if (__lane_id() == 0 && m) atomicAdd(n_live, (int)__popcll(m));
+    }
 }
 
 // ===========================================================================
@@ -2894,7 +2914,7 @@ mops_status mops_order_particles(const mops_mesh* mesh, int64_t n, const int32_t
     uint64_t* kout = (uint64_t*)(base + a8);
     int* vin = (int*)(base + 2 * a8);
     void* tmp = base + 2 * a8 + a4;
-    particle_key_kernel<<<grid_for(n), kBlock, 0, s>>>(n, mesh->C, d_cell, nullptr, mesh->d_cell_key, kin, vin);
+    particle_key_kernel<<<grid_for(n), kBlock, 0, s>>>(n, mesh->C, d_cell, nullptr, mesh->d_cell_key, kin, vin, nullptr);
     HIP_TRY(hipGetLastError());
     HIP_TRY(hipcub::DeviceRadixSort::SortPairs(tmp, tmp_bytes, kin, kout, vin, d_order, (int)n, 0, 64, s));
     return MOPS_OK;
@@ -2912,10 +2932,14 @@ int64_t mops_order_scratch_bytes(int64_t n) {
 }
 
 mops_status mops_order_particles_live(const mops_mesh* mesh, int64_t n, const int32_t* d_cell, const int32_t* d_death,
-                                      int32_t* d_order, void* d_scratch, int64_t scratch_bytes, void* stream) {
+                                      int32_t* d_order, int32_t* d_n_live, void* d_scratch, int64_t scratch_bytes,
+                                      void* stream) {
     if (!mesh || n < 0 || (n > 0 && (!d_cell || !d_order || !d_scratch)) || n >= INT32_MAX)
         return fail(MOPS_ERR_INVALID, "mops_order_particles_live: invalid argument");
-    if (n == 0) return MOPS_OK;
+    if (n == 0) {
+        if (d_n_live) HIP_TRY(hipMemsetAsync(d_n_live, 0, sizeof(int32_t), (hipStream_t)stream));
+        return MOPS_OK;
+    }
     const int64_t need = mops_order_scratch_bytes(n);
     if (need <= 0 || scratch_bytes < need)
         return fail(MOPS_ERR_INVALID, "mops_order_particles_live: scratch smaller than mops_order_scratch_bytes(n)");
@@ -2929,7 +2953,8 @@ mops_status mops_order_particles_live(const mops_mesh* mesh, int64_t n, const in
     uint64_t* kout = (uint64_t*)(base + a8);
     int* vin = (int*)(base + 2 * a8);
     void* tmp = base + 2 * a8 + a4;
-    particle_key_kernel<<<grid_for(n), kBlock, 0, s>>>(n, mesh->C, d_cell, d_death, mesh->d_cell_key, kin, vin);
+    if (d_n_live) HIP_TRY(hipMemsetAsync(d_n_live, 0, sizeof(int32_t), s));
+    particle_key_kernel<<<grid_for(n), kBlock, 0, s>>>(n, mesh->C, d_cell, d_death, mesh->d_cell_key, kin, vin, d_n_live);
     HIP_TRY(hipGetLastError());
     HIP_TRY(hipcub::DeviceRadixSort::SortPairs(tmp, tmp_bytes, kin, kout, vin, d_order, (int)n, 0, 64, s));
     return MOPS_OK;
@@ -2970,6 +2995,7 @@ mops_status mops_traj_advance(const mops_mesh* mesh, const mops_field* front, co
     a.mono0 = front->d_mono;
     a.mono1 = back ? back->d_mono : front->d_mono;
     a.order = p->d_order;
+    a.n_live = p->d_n_live;
     a.cellB = mesh->d_cellB;
     a.px = p->d_x; a.py = p->d_y; a.pz = p->d_z; a.depth = p->d_depth; a.cell = p->d_cell; a.death = p->d_death_step;
     a.n = p->n;
@@ -3127,7 +3153,7 @@ mops_status mops_run_trajectories(const mops_mesh* mesh, const mops_field* front
         if (e != hipSuccess) { st = fail(MOPS_ERR_HIP, hipGetErrorString(e)); break; }
         if ((st = dmalloc(&order, (size_t)n, nullptr)) != MOPS_OK) break;
         if ((st = mops_order_particles(mesh, n, cells, order, stream)) != MOPS_OK) break;
-        mops_particles prt{n, x, y, z, dep, cells, death, order};
+        mops_particles prt{n, x, y, z, dep, cells, death, order, nullptr};
         if ((st = mops_traj_advance(mesh, front, back, cfg, &prt, 0, n_steps, rec, n, stream)) != MOPS_OK) break;
         if ((st = mops_traj_finalize(n, K, seeds, rec, n, back ? 1 : 0, nullptr, pts, vel, tmp, sal, last, stream)) !=
             MOPS_OK)

@@ -286,6 +286,7 @@ class ParticleSet:
         # finalize() writes line ids[slot], so outputs keep the seed order
         self.ids = torch.arange(self.n, dtype=torch.int32, device=dev)
         self._compact_scratch = {}
+        self._n_live = {}  # (lo, hi) -> device int32: live particles at the front of the range after compact()
         self._written = False
         self._c = cfg.ctype()
         self.reorder(stream=torch.cuda.current_stream(dev).cuda_stream)
@@ -339,10 +340,14 @@ class ParticleSet:
             with torch.cuda.stream(s):
                 self._compact_scratch[key] = torch.empty((nb,), dtype=torch.uint8, device=self.seeds.device)
         scratch = self._compact_scratch[key]
+        if key not in self._n_live:
+            with torch.cuda.stream(s):
+                self._n_live[key] = torch.zeros((1,), dtype=torch.int32, device=self.seeds.device)
         e4 = 4
         L.check(lib.mops_order_particles_live(self.mesh.handle, n, C.c_void_p(self.cell.data_ptr() + e4 * lo),
                                               C.c_void_p(self.death.data_ptr() + e4 * lo),
                                               C.c_void_p(self.order.data_ptr() + e4 * lo),
+                                              C.c_void_p(self._n_live[key].data_ptr()),
                                               C.c_void_p(scratch.data_ptr()), scratch.numel(), _stream_handle(s)),
                 "mops_order_particles_live")
         with torch.cuda.stream(s):
@@ -392,7 +397,7 @@ class ParticleSet:
 
     def particles(self) -> L.Particles:
         return L.Particles(self.n, self.x.data_ptr(), self.y.data_ptr(), self.z.data_ptr(), self.depth.data_ptr(),
-                           self.cell.data_ptr(), self.death.data_ptr(), None)  # physically ordered: no indirection
+                           self.cell.data_ptr(), self.death.data_ptr(), None, None)  # physically ordered
 
     def advance(self, front: DeviceField, back: DeviceField | None, step_begin: int, step_end: int, stream=None):
         p = self.particles()
@@ -402,11 +407,14 @@ class ParticleSet:
         L.check(st, "mops_traj_advance")
         self._written = True
 
-    def _sub_particles(self, lo: int, hi: int) -> L.Particles:
+    def _sub_particles(self, lo: int, hi: int, live_count=None) -> L.Particles:
+        """Slots [lo, hi) as a launch argument; ``live_count``: the range's device live count after a
+        compaction (only its leading live slots are launched over the XCDs)."""
         e4, e8 = 4, 8
         return L.Particles(hi - lo, self.x.data_ptr() + e8 * lo, self.y.data_ptr() + e8 * lo,
                            self.z.data_ptr() + e8 * lo, self.depth.data_ptr() + e4 * lo,
-                           self.cell.data_ptr() + e4 * lo, self.death.data_ptr() + e4 * lo, None)
+                           self.cell.data_ptr() + e4 * lo, self.death.data_ptr() + e4 * lo, None,
+                           None if live_count is None else live_count.data_ptr())
 
     def advance_pipelined(self, front: DeviceField, back: DeviceField | None, step_begin: int, step_end: int,
                           streams, chunks: int, timing=None, compact: bool = False, compact_priority: bool = False):
@@ -459,7 +467,7 @@ class ParticleSet:
                 if timing is not None:
                     e0 = torch.cuda.Event(enable_timing=True); e1 = torch.cuda.Event(enable_timing=True)
                     e0.record(st)
-                p = self._sub_particles(lo, hi)
+                p = self._sub_particles(lo, hi, self._n_live.get((lo, hi)) if (compact and t > 0) else None)
                 rc = lib.mops_traj_advance(self.mesh.handle, front.handle, None if back is None else back.handle,
                                            C.byref(self._c), C.byref(p), tb[t], tb[t + 1],
                                            C.c_void_p(self.records.data_ptr() + 8 * lo), self.n,
