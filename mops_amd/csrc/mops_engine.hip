@@ -1557,6 +1557,68 @@ __global__ void __launch_bounds__(256) assemble_kernel(int64_t n, int64_t K, con
     }
 }
 
+// Assembly and NaN cleanup in one pass when a line's K records fit the block's LDS tile (K <=
+// kAsmFull: every record period of a day's run at 1 h records): the whole [K][6][32-slot] slab
+// plus the seeds is staged, each line's first non-finite point found there, and the cleaned
+// line -- RemoveNaNTrajectoriesAndReindex's padding with the last finite point, zeroed velocity
+// from the point before it, temperature/salinity held (TrajectoryCommon.h:92-121) -- written
+// once, with consecutive threads on consecutive doubles of a line (whole 600-B point runs at K =
+// 24 instead of 192-B chunks), saving remove_nan_kernel's second, strided pass over the lines.
+constexpr int kAsmFull = 24;
+__global__ void __launch_bounds__(256) assemble_clean_kernel(int64_t n, int K, const double* __restrict__ seeds,
+                                                             const double* __restrict__ rec, int64_t stride,
+                                                             int pathline, const int32_t* __restrict__ line,
+                                                             double* __restrict__ pts, double* __restrict__ vel,
+                                                             double* __restrict__ tmp, double* __restrict__ sal,
+                                                             double* __restrict__ last) {
+    __shared__ double tile[kAsmFull][6][kAsmSlots + 1];
+    __shared__ double seed[kAsmSlots][3];
+    __shared__ int64_t row[kAsmSlots];
+    __shared__ int cut[kAsmSlots];
+    const int t = threadIdx.x;
+    const int64_t s0 = (int64_t)blockIdx.x * kAsmSlots;
+    const int ns = (int)((n - s0) < kAsmSlots ? (n - s0) : kAsmSlots);
+    const int P = K + 1;
+    for (int e = t; e < K * 6 * kAsmSlots; e += blockDim.x) {
+        const int i = e % kAsmSlots, c = (e / kAsmSlots) % 6, kk = e / (kAsmSlots * 6);
+        if (i < ns) tile[kk][c][i] = rec[kk * 6 * stride + c * stride + s0 + i];
+    }
+    for (int e = t; e < 3 * kAsmSlots; e += blockDim.x)
+        if (e / 3 < ns) seed[e / 3][e % 3] = seeds[3 * s0 + e];
+    if (t < ns) row[t] = line ? (int64_t)line[s0 + t] : s0 + t;
+    __syncthreads();
+    // original point j of line i: seed, then the records' positions
+    auto point = [&](int i, int j, int c) -> double { return j == 0 ? seed[i][c] : tile[j - 1][c][i]; };
+    if (t < ns) {
+        int k = 0;
+        for (; k < P; ++k)
+            if (!finite3(point(t, k, 0), point(t, k, 1), point(t, k, 2))) break;
+        cut[t] = k;
+    }
+    __syncthreads();
+    for (int e = t; e < ns * P * 3; e += blockDim.x) {  // points (and velocities)
+        const int i = e / (P * 3), off = e - i * (P * 3), j = off / 3, c = off - j * 3, k = cut[i];
+        const int64_t o = 3 * row[i] * P + off;
+        pts[o] = (k < P && (k == 0 || j >= k)) ? point(i, k == 0 ? 0 : k - 1, c) : point(i, j, c);
+        if (vel) vel[o] = (j == K || (k < P && (k == 0 || j >= k - 1))) ? 0.0 : tile[j][3 + c][i];
+    }
+    if (tmp || sal) {
+        for (int e = t; e < ns * P; e += blockDim.x) {
+            const int i = e / P, j = e - i * P, k = cut[i];
+            const int src = (k < P && (k == 0 || j >= k)) ? (k == 0 ? 0 : k - 1) : j;  // held value's index
+            const int64_t o = row[i] * P + j;
+            if (tmp) tmp[o] = (pathline && src < K) ? tile[src][3][i] : 0.0;
+            if (sal) sal[o] = (pathline && src < K) ? tile[src][4][i] : 0.0;
+        }
+    }
+    if (last) {
+        for (int e = t; e < ns * 3; e += blockDim.x) {
+            const int i = e / 3, c = e - i * 3, k = cut[i];
+            last[3 * row[i] + c] = (k < P) ? point(i, k == 0 ? 0 : k - 1, c) : point(i, K, c);  // line order
+        }
+    }
+}
+
 // ===========================================================================
 // derived-field preprocessing (once per snapshot)
 // ===========================================================================
@@ -3033,10 +3095,15 @@ mops_status mops_traj_finalize(int64_t n, int64_t K, const double* d_seeds, cons
         return fail(MOPS_ERR_INVALID, "mops_traj_finalize: invalid argument");
     if (n == 0) return MOPS_OK;
     hipStream_t s = (hipStream_t)stream;
-    assemble_kernel<<<(unsigned)((n + kAsmSlots - 1) / kAsmSlots), 256, 0, s>>>(n, K, d_seeds, d_records, stride,
-                                                                               pathline, d_line, d_points, d_vel,
-                                                                               d_tmp, d_sal);
-    remove_nan_kernel<<<grid_for(n), kBlock, 0, s>>>(n, K + 1, nullptr, d_points, d_vel, d_tmp, d_sal, d_last);
+    const unsigned nb = (unsigned)((n + kAsmSlots - 1) / kAsmSlots);
+    if (K <= kAsmFull) {
+        assemble_clean_kernel<<<nb, 256, 0, s>>>(n, (int)K, d_seeds, d_records, stride, pathline, d_line, d_points,
+                                                 d_vel, d_tmp, d_sal, d_last);
+    } else {
+        assemble_kernel<<<nb, 256, 0, s>>>(n, K, d_seeds, d_records, stride, pathline, d_line, d_points, d_vel, d_tmp,
+                                           d_sal);
+        remove_nan_kernel<<<grid_for(n), kBlock, 0, s>>>(n, K + 1, nullptr, d_points, d_vel, d_tmp, d_sal, d_last);
+    }
     HIP_TRY(hipGetLastError());
     return MOPS_OK;
 }
