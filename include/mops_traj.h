@@ -206,6 +206,21 @@ mops_status mops_locate_cells_hinted(const mops_mesh* mesh, int64_t n, const dou
 mops_status mops_order_particles(const mops_mesh* mesh, int64_t n, const int32_t* d_cell, int32_t* d_order,
                                  void* stream);
 
+/* Out-of-place gather of particle arrays by a slot order, all in one launch
+ * (no reference counterpart: the locality order is the engine's own):
+ * dst[row][i] = src[row][d_order[i]] for i < n (d_order NULL = copy), for up
+ * to 16 arrays of 4-, 8- or 24-byte elements, each with `rows` rows
+ * `row_stride` elements apart (e.g. the [K][6][stride] record slab). */
+typedef struct {
+    const void* d_src;
+    void* d_dst;                         /* must differ from d_src */
+    int64_t elem_bytes;                  /* 4, 8 or 24 */
+    int64_t rows;                        /* >= 1 */
+    int64_t row_stride;                  /* elements between rows (>= n when rows > 1) */
+} mops_perm_array;
+mops_status mops_permute_arrays(int64_t n, const int32_t* d_order, int32_t count, const mops_perm_array* arrays,
+                                void* stream);
+
 /* Dead-particle compaction (no reference counterpart: the reference's
  * parallel_for keeps visiting particles whose lambda has returned,
  * MPASOVisualizerKernels.cpp:944-957, quirk Q1).  As mops_order_particles,

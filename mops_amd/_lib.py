@@ -19,7 +19,7 @@ EXPORTED = (
     "mops_field_create", "mops_field_create_device", "mops_field_rebuild_device", "mops_field_create_derived", "mops_field_export", "mops_cell_to_vertex_attr",
     "mops_field_destroy", "mops_field_bytes",
     "mops_locate_cells", "mops_locate_cells_hinted", "mops_order_particles", "mops_order_scratch_bytes",
-    "mops_order_particles_live",
+    "mops_order_particles_live", "mops_permute_arrays",
     "mops_traj_num_records", "mops_traj_num_steps", "mops_traj_advance", "mops_traj_finalize",
     "mops_remove_nan_lines", "mops_remove_nan_ragged", "mops_run_trajectories", "mops_build_id",
     # include/mops_io.h
@@ -57,6 +57,11 @@ class Particles(C.Structure):
     _fields_ = [("n", C.c_int64), ("d_x", C.c_void_p), ("d_y", C.c_void_p), ("d_z", C.c_void_p),
                 ("d_depth", C.c_void_p), ("d_cell", C.c_void_p), ("d_death_step", C.c_void_p),
                 ("d_order", C.c_void_p), ("d_n_live", C.c_void_p)]
+
+
+class PermArray(C.Structure):
+    _fields_ = [("d_src", C.c_void_p), ("d_dst", C.c_void_p), ("elem_bytes", C.c_int64), ("rows", C.c_int64),
+                ("row_stride", C.c_int64)]
 
 
 class MopsError(RuntimeError):
@@ -138,6 +143,7 @@ def load(path: str | None = None):
     lib.mops_remove_nan_lines.argtypes = [I64, I64, P, P, P, P, P, P]; lib.mops_remove_nan_lines.restype = st
     lib.mops_remove_nan_ragged.argtypes = [I64, P, P, P, P, P, P, P]; lib.mops_remove_nan_ragged.restype = st
     lib.mops_order_scratch_bytes.argtypes = [I64]; lib.mops_order_scratch_bytes.restype = I64
+    lib.mops_permute_arrays.argtypes = [I64, P, I32, P, P]; lib.mops_permute_arrays.restype = st
     lib.mops_order_particles_live.argtypes = [P, I64, P, P, P, P, P, I64, P]
     lib.mops_order_particles_live.restype = st
     lib.mops_run_trajectories.argtypes = [P, P, P, P, I64, P, P, C.c_float, P, P, P, P, P, P, P, P, P, P]

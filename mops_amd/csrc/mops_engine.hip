@@ -2310,6 +2310,38 @@ __global__ void particle_key_kernel(int64_t n, int64_t C, const int* cell, const
     }
 }
 
+// Gather of up to kPermMax SoA arrays (and record rows) by a slot order in one launch:
+// dst[row][i] = src[row][order[i]] (order NULL = copy); blockIdx.y enumerates (array, row).
+constexpr int kPermMax = 16;
+struct PermArrays {
+    const char* src[kPermMax];
+    char* dst[kPermMax];
+    int64_t stride_bytes[kPermMax];  // bytes between consecutive rows
+    int elem[kPermMax];              // bytes per element: 4, 8 or 24
+    int row0[kPermMax + 1];          // first blockIdx.y row of each array (prefix over rows)
+    int count;
+};
+__global__ void permute_kernel(int64_t n, const int32_t* __restrict__ order, PermArrays a) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const int y = blockIdx.y;
+    int k = 0;
+    while (k + 1 < a.count && a.row0[k + 1] <= y) ++k;  // the array this row belongs to (uniform)
+    const int64_t r = y - a.row0[k];
+    const int64_t j = order ? (int64_t)order[i] : i;
+    const char* src = a.src[k] + r * a.stride_bytes[k];
+    char* dst = a.dst[k] + r * a.stride_bytes[k];
+    switch (a.elem[k]) {
+        case 4: reinterpret_cast<int32_t*>(dst)[i] = reinterpret_cast<const int32_t*>(src)[j]; break;
+        case 8: reinterpret_cast<double*>(dst)[i] = reinterpret_cast<const double*>(src)[j]; break;
+        default: {
+            const double* q = reinterpret_cast<const double*>(src) + 3 * j;
+            double* o = reinterpret_cast<double*>(dst) + 3 * i;
+            o[0] = q[0]; o[1] = q[1]; o[2] = q[2];
+        }
+    }
+}
+
 // ===========================================================================
 // host side
 // ===========================================================================
@@ -2991,6 +3023,34 @@ int64_t mops_order_scratch_bytes(int64_t n) {
         return 0;
     const size_t a8 = ((size_t)n * 8 + 255) / 256 * 256, a4 = ((size_t)n * 4 + 255) / 256 * 256;
     return (int64_t)(2 * a8 + a4 + tmp_bytes + 256);
+}
+
+mops_status mops_permute_arrays(int64_t n, const int32_t* d_order, int32_t count, const mops_perm_array* arrays,
+                                void* stream) {
+    if (n < 0 || count < 0 || count > kPermMax || (count > 0 && !arrays))
+        return fail(MOPS_ERR_INVALID, "mops_permute_arrays: invalid argument");
+    if (n == 0 || count == 0) return MOPS_OK;
+    PermArrays a{};
+    a.count = count;
+    int rows = 0;
+    for (int k = 0; k < count; ++k) {
+        const mops_perm_array& d = arrays[k];
+        if (!d.d_src || !d.d_dst || (d.elem_bytes != 4 && d.elem_bytes != 8 && d.elem_bytes != 24) || d.rows < 1 ||
+            (d.rows > 1 && d.row_stride < n) || d.d_src == d.d_dst)
+            return fail(MOPS_ERR_INVALID, "mops_permute_arrays: bad array descriptor (out of place, 4/8/24-B elements)");
+        a.src[k] = static_cast<const char*>(d.d_src);
+        a.dst[k] = static_cast<char*>(d.d_dst);
+        a.elem[k] = (int)d.elem_bytes;
+        a.stride_bytes[k] = d.row_stride * d.elem_bytes;
+        a.row0[k] = rows;
+        rows += (int)d.rows;
+        if (rows > 65535) return fail(MOPS_ERR_INVALID, "mops_permute_arrays: more than 65535 rows");
+    }
+    a.row0[count] = rows;
+    const dim3 grid((unsigned)((n + kBlock - 1) / kBlock), (unsigned)rows);
+    permute_kernel<<<grid, kBlock, 0, (hipStream_t)stream>>>(n, d_order, a);
+    HIP_TRY(hipGetLastError());
+    return MOPS_OK;
 }
 
 mops_status mops_order_particles_live(const mops_mesh* mesh, int64_t n, const int32_t* d_cell, const int32_t* d_death,

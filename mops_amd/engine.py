@@ -286,6 +286,7 @@ class ParticleSet:
         # finalize() writes line ids[slot], so outputs keep the seed order
         self.ids = torch.arange(self.n, dtype=torch.int32, device=dev)
         self._compact_scratch = {}
+        self._spare = {}  # second buffers for the permutations (_apply_order)
         self._n_live = {}  # (lo, hi) -> device int32: live particles at the front of the range after compact()
         self._written = False
         self._c = cfg.ctype()
@@ -299,18 +300,47 @@ class ParticleSet:
                 "mops_order_particles")
         if not self.use_order or self.n == 0:
             return
+        self._apply_order(self.order, 0, self.n, stream, self.records.shape[0] if self._written else 0)
+
+    _STATE = (("x", 8), ("y", 8), ("z", 8), ("depth", 4), ("cell", 4), ("death", 4), ("ids", 4), ("seeds", 24))
+
+    def _apply_order(self, order, lo: int, hi: int, stream, record_slots: int):
+        """Permute slots [lo, hi) of the SoA state, seeds, slot ids and the first ``record_slots`` record
+        slots by ``order`` (local indices) with one mops_permute_arrays launch into the spare buffers;
+        the whole set swaps buffers, a sub-range is copied back with a second launch."""
         torch = self.torch
+        n = hi - lo
+        if n <= 0:
+            return
         if isinstance(stream, int):
-            s = torch.cuda.ExternalStream(stream) if stream else None
+            s = torch.cuda.ExternalStream(stream) if stream else torch.cuda.current_stream(self.seeds.device)
         else:
-            s = stream
-        with torch.cuda.stream(s) if s is not None else _nullcontext():
-            o = self.order.long()
-            for t in (self.x, self.y, self.z, self.depth, self.cell, self.death, self.ids):
-                t.copy_(t[o])
-            self.seeds.copy_(self.seeds[o])
-            if self._written:
-                self.records.copy_(self.records[:, :, o])
+            s = stream if stream is not None else torch.cuda.current_stream(self.seeds.device)
+        names = [(k, e) for k, e in self._STATE] + ([("records", 8)] if record_slots > 0 else [])
+        with torch.cuda.stream(s):
+            for k, _ in names:
+                if k not in self._spare:  # (allocated on first use, then kept)
+                    self._spare[k] = torch.empty_like(getattr(self, k))
+
+        def desc(src, dst, name, eb):
+            if name == "records":
+                return L.PermArray(src.data_ptr() + 8 * lo, dst.data_ptr() + 8 * lo, 8, int(record_slots) * 6, self.n)
+            return L.PermArray(src.data_ptr() + eb * lo, dst.data_ptr() + eb * lo, eb, 1, n)
+
+        lib = L.load()
+        arr = (L.PermArray * len(names))(*[desc(getattr(self, k), self._spare[k], k, e) for k, e in names])
+        L.check(lib.mops_permute_arrays(n, C.c_void_p(order.data_ptr() + 4 * lo), len(names), arr, _stream_handle(s)),
+                "mops_permute_arrays")
+        if lo == 0 and hi == self.n:
+            for k, _ in names:  # the gathered copies become the state
+                cur = getattr(self, k)
+                setattr(self, k, self._spare[k])
+                self._spare[k] = cur
+            if record_slots > 0 and record_slots < self.records.shape[0]:
+                self.records[record_slots:].zero_()  # (the spare slab's unwritten slots must be zero)
+        else:
+            back = (L.PermArray * len(names))(*[desc(self._spare[k], getattr(self, k), k, e) for k, e in names])
+            L.check(lib.mops_permute_arrays(n, None, len(names), back, _stream_handle(s)), "mops_permute_arrays")
 
     def original(self, t):
         """A per-slot tensor back in the particles' seed order."""
@@ -350,15 +380,7 @@ class ParticleSet:
                                               C.c_void_p(self._n_live[key].data_ptr()),
                                               C.c_void_p(scratch.data_ptr()), scratch.numel(), _stream_handle(s)),
                 "mops_order_particles_live")
-        with torch.cuda.stream(s):
-            o = self.order[lo:hi].long()
-            for t in (self.x, self.y, self.z, self.depth, self.cell, self.death, self.ids):
-                t[lo:hi].copy_(t[lo:hi][o])
-            self.seeds[lo:hi].copy_(self.seeds[lo:hi][o])
-            k = min(int(records_written), self.records.shape[0])
-            if k > 0:
-                r = self.records[:k, :, lo:hi]
-                r.copy_(r[:, :, o])
+        self._apply_order(self.order, lo, hi, s, min(int(records_written), self.records.shape[0]))
 
     def reset(self, depth=None):
         self.x.copy_(self.seeds[:, 0]); self.y.copy_(self.seeds[:, 1]); self.z.copy_(self.seeds[:, 2])
