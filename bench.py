@@ -93,6 +93,9 @@ def parse():
     p.add_argument("--compact", choices=["auto", "on", "off"], default="auto",
                    help="config 2: re-sort each particle part with its dead particles last between step chunks "
                         "(ParticleSet.compact); auto = on for RK4 (quirk Q1 kills half the particles in a day)")
+    p.add_argument("--finalize", choices=["parts", "after"], default="parts",
+                   help="config 2: assemble each particle part's lines on its own stream after its last chunk "
+                        "(parts, overlapping the other parts' final waves) or all lines once every part is done")
     p.add_argument("--compact-priority", action="store_true",
                    help="run the compaction re-sorts on high-priority streams (experiment)")
     p.add_argument("--no-cpu-baseline", action="store_true")
@@ -398,6 +401,19 @@ def main():
                 e1.record(compute)
                 if timed:
                     kernel_ms.append((e0, e1))
+                if (s0, s1) == segments[-1]:
+                    # the reference's StreamLine ends by assembling the lines (FinalizeTrajectoryLines +
+                    # RemoveNaN, MPASOVisualizerKernels.cpp:1005-1014), part of every call: each particle
+                    # part's lines on its own stream, overlapping the other parts' final waves
+                    fin = []
+                    if args.finalize == "parts":
+                        lines_out[0] = ps_.finalize(pathline, streams=part_streams, timing=fin)
+                        for st in part_streams:
+                            j = torch.cuda.Event(); j.record(st); compute.wait_event(j)
+                    else:
+                        lines_out[0] = ps_.finalize(pathline, stream=compute, timing=fin)
+                    if timed:
+                        finalize_ms.append(fin)
                 if gather_records:  # the records this segment completed, gathered while the next one computes
                     k0, k1 = s0 // period, min(s1 // period, ps_.K)
                     if k1 > k0:
@@ -407,14 +423,6 @@ def main():
                         with torch.cuda.stream(comm):
                             for k in range(k0, k1):
                                 all_gather_flat(dist, gathered[k].view(-1), ps_.records[k].view(-1), args.backend)
-            # the reference's StreamLine ends by assembling the lines (FinalizeTrajectoryLines +
-            # RemoveNaN, MPASOVisualizerKernels.cpp:1005-1014): part of every call
-            f0 = torch.cuda.Event(enable_timing=True); f1 = torch.cuda.Event(enable_timing=True)
-            f0.record(compute)
-            lines_out[0] = ps_.finalize(pathline, stream=compute)
-            f1.record(compute)
-            if timed:
-                finalize_ms.append((f0, f1))
             if world > 1:  # the checkpoint: every particle's final state on every rank
                 if ev_ckpt[0] is not None:  # the previous call's checkpoint gather has read ckpt
                     compute.wait_event(ev_ckpt[0])
@@ -497,7 +505,7 @@ def main():
                               f"{args.parts * args.chunks} overlapping traj_kernel launches)")
     roof["dispatches_per_unit"] = len(dms) / max(1, args.steps * len(segments))
     roof["avg_dispatch_ms"] = (sum(dms) / len(dms)) if dms else None  # = rocprofv3's traj_kernel average
-    fms = [a.elapsed_time(b) for (a, b) in finalize_ms]
+    fms = [sum(a.elapsed_time(b) for (a, b) in call) for call in finalize_ms]  # part launches per call
     finalize_avg = (sum(fms) / len(fms)) if fms else None
 
     cpu = None
@@ -542,10 +550,12 @@ def main():
             "nominal_particle_steps_per_call": n_all * n_steps,
             "attempted_particle_steps_per_call": attempted_all,
             "dead_fraction": dead_all / max(n_all, 1),
-            "finalize": {"ms_per_call": finalize_avg,
+            "finalize": {"ms_per_call": finalize_avg, "mode": args.finalize,
                          "share_of_step": (finalize_avg / (elapsed / args.steps * 1e3)) if finalize_avg else None,
-                         "what": "line assembly + NaN cleanup on device (assemble_kernel + remove_nan_kernel), "
-                                 "inside every timed call as in the reference's StreamLine"},
+                         "what": "line assembly + NaN cleanup on device (assemble_clean_kernel, or assemble_kernel + "
+                                 "remove_nan_kernel past 24 records), inside every timed call as in the reference's "
+                                 "StreamLine: one launch per particle part on its stream (ms_per_call sums them), "
+                                 "overlapping the other parts' final waves"},
             "dead_particle_compaction": compact,
             "roofline": roof,
             "cpu_baseline": cpu,

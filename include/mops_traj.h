@@ -233,6 +233,12 @@ int64_t mops_order_scratch_bytes(int64_t n);
 mops_status mops_order_particles_live(const mops_mesh* mesh, int64_t n, const int32_t* d_cell,
                                       const int32_t* d_death, int32_t* d_order, int32_t* d_n_live,
                                       void* d_scratch, int64_t scratch_bytes, void* stream);
+/* Zero record slots [k_begin, K) of slots [*d_n_live, n) (d_records [K][6][record_stride]):
+ * after a compaction that moved only the sampled slots [0, k_begin), the dead particles now
+ * at the end carry the zeros of their unsampled slots again (see mops_traj_advance).  No
+ * reference counterpart (the reference never re-sorts). */
+mops_status mops_records_clear_dead(int64_t n, const int32_t* d_n_live, int64_t k_begin, int64_t K,
+                                    double* d_records, int64_t record_stride, void* stream);
 
 /* ---- trajectory hot path (device-resident) ----------------------------- */
 
@@ -247,9 +253,16 @@ int64_t mops_traj_num_steps(const mops_traj_cfg* cfg);
  * 874-1003) or PathLine (Kernel::PathLine, :1329-1483) call.  Records go to
  * d_records laid out [K][6][record_stride] doubles (px,py,pz,vx,vy,vz);
  * slot 0 also receives the seed / first-step velocity pre-writes
- * (:901, :990).  The caller zero-fills d_records before step 0 (the
- * reference's vector::resize zero-init).  Calling it over consecutive step
- * ranges is identical to one call over [0, n_steps). */
+ * (:901, :990).  d_records needs no initialisation when the calls start at
+ * step 0: every slot a particle does not sample (after its death, past the
+ * run's last record step, or all of them for a particle already dead at step
+ * 0) is written with the zeros of the reference's vector::resize zero-init --
+ * at its death or by the call that reaches n_steps.  A caller whose
+ * first call starts after step 0 passes records zero-filled.  Calling it over
+ * consecutive step ranges is identical to one call over [0, n_steps); a
+ * caller that moves particles between slots in between (a re-sort) moves
+ * every record slot, or clears the moved dead particles' unsampled slots
+ * (mops_records_clear_dead). */
 mops_status mops_traj_advance(const mops_mesh* mesh, const mops_field* front, const mops_field* back,
                               const mops_traj_cfg* cfg, const mops_particles* particles,
                               int64_t step_begin, int64_t step_end, double* d_records,

@@ -19,7 +19,7 @@ EXPORTED = (
     "mops_field_create", "mops_field_create_device", "mops_field_rebuild_device", "mops_field_create_derived", "mops_field_export", "mops_cell_to_vertex_attr",
     "mops_field_destroy", "mops_field_bytes",
     "mops_locate_cells", "mops_locate_cells_hinted", "mops_order_particles", "mops_order_scratch_bytes",
-    "mops_order_particles_live", "mops_permute_arrays",
+    "mops_order_particles_live", "mops_permute_arrays", "mops_records_clear_dead",
     "mops_traj_num_records", "mops_traj_num_steps", "mops_traj_advance", "mops_traj_finalize",
     "mops_remove_nan_lines", "mops_remove_nan_ragged", "mops_run_trajectories", "mops_build_id",
     # include/mops_io.h
@@ -146,6 +146,8 @@ def load(path: str | None = None):
     lib.mops_permute_arrays.argtypes = [I64, P, I32, P, P]; lib.mops_permute_arrays.restype = st
     lib.mops_order_particles_live.argtypes = [P, I64, P, P, P, P, P, I64, P]
     lib.mops_order_particles_live.restype = st
+    lib.mops_records_clear_dead.argtypes = [I64, P, I64, I64, P, I64, P]
+    lib.mops_records_clear_dead.restype = st
     lib.mops_run_trajectories.argtypes = [P, P, P, P, I64, P, P, C.c_float, P, P, P, P, P, P, P, P, P, P]
     lib.mops_run_trajectories.restype = st
     _lib = lib

@@ -38,7 +38,7 @@
 #include "mops_io.h"
 #include "mops_traj.h"
 
-#define MOPS_ABI_VERSION 3
+#define MOPS_ABI_VERSION 4
 #ifndef MOPS_BUILD_ID
 #define MOPS_BUILD_ID "unstamped"  // __graft_entry__.build_engine passes the sources' identity (mops_build_id)
 #endif
@@ -95,7 +95,7 @@ struct mops_mesh {
     uint64_t* d_hkeys = nullptr;  // [H] key or ~0 (empty)
     int2* d_hval = nullptr;       // [H]
     uint32_t hmask = 0;           // H - 1
-    uint64_t* d_cell_key = nullptr;  // Morton key of each cell centre (particle locality order)
+    uint32_t* d_cell_rank = nullptr;  // rank of each cell in the Morton order of the centres (particle locality order)
     double* d_cellB = nullptr;       // [C][maxv] Wachspress B_i of each cell polygon
     double* d_rloc2 = nullptr;       // [C] squared hinted-locate radius (locate_radius_kernel)
     double* d_ring = nullptr;        // [C] hinted-locate ring distance (locate_radius_kernel)
@@ -142,7 +142,26 @@ struct mops_field {
 // ===========================================================================
 // device helpers -- every expression keeps the reference's evaluation order
 // ===========================================================================
+// ISA markers for instruction counting (tools/isa_marks.py; -DMOPS_ISA_MARKS builds only, never a
+// product build): an assembly comment "@@MARK <id>" at the marked point
+#if defined(MOPS_ISA_MARKS)
+#define MOPS_MARK(id) asm volatile("; @@MARK %0" ::"i"(id))
+#else
+#define MOPS_MARK(id) do { } while (0)
+#endif
+
 namespace dev {
+
+// Zeros of records [k0, K) of one particle (records [K][6][stride]): what the reference's
+// preallocated trajectory holds past a particle's death (the lambda returns, those points are
+// never assigned) -- written once, at the death, instead of a memset of every record per run
+__device__ __forceinline__ void clear_records(double* rec, int64_t stride, int64_t pid, int64_t k0, int64_t K) {
+    for (int64_t k = k0; k < K; ++k) {
+        double* rk = rec + k * 6 * stride + pid;
+#pragma unroll
+        for (int c = 0; c < 6; ++c) rk[c * stride] = 0.0;
+    }
+}
 
 #if defined(MOPS_WAVE_STAMPS)
 // Diagnostic builds only (tools/build_variant.sh -DMOPS_WAVE_STAMPS): 8 words per
@@ -565,6 +584,7 @@ __device__ __forceinline__ bool weights(const Cell<MAXV>& c, int L, int V, doubl
     // order of the edges is immaterial) and the arguments of A_i = area(poly[i-1], poly[i], p)
     // (Interpolation.hpp:137-165: A_0 = area(poly[N-1], poly[0], p), A_{i+1} = area(poly[i], poly[i+1], p));
     // A_i is kept in w[i] until the weights are formed
+    MOPS_MARK(200 + NV);
     bool inside = true;
 #pragma unroll
     for (int i = 0; i < MAXV; ++i) {
@@ -588,6 +608,7 @@ __device__ __forceinline__ bool weights(const Cell<MAXV>& c, int L, int V, doubl
             w[i] = 0.0;
         }
     }
+    MOPS_MARK(210 + NV);
     if (!inside) return false;
     // (the reference also range-checks the vertex ids in its zTop loop, :776-779; mops_mesh_create
     // rejects a mesh with an out-of-range active verticesOnCell entry, so that test always passes)
@@ -606,6 +627,7 @@ __device__ __forceinline__ bool weights(const Cell<MAXV>& c, int L, int V, doubl
 #pragma unroll
     for (int i = 0; i < MAXV; ++i)
         if (i < nv) w[i] *= recp;
+    MOPS_MARK(220 + NV);
     return true;
 }
 
@@ -970,6 +992,7 @@ struct Pair {
 template <int MAXV, int GR, int NV>
 __device__ __forceinline__ void pair_sums(const Cell<MAXV>& c, const double* w, const double* __restrict__ pr, int L,
                                           int k, Pair& S) {
+    MOPS_MARK(300 + NV);
     S.zm = S.zk = S.wm = S.wk = 0.0;
     S.um0 = S.um1 = S.um2 = S.uk0 = S.uk1 = S.uk2 = 0.0;
     // 32-bit record indices: V * L < 2^31 (mops_mesh_create), so v*(L-1) + k - 1 fits
@@ -1010,6 +1033,7 @@ __device__ __forceinline__ void pair_sums(const Cell<MAXV>& c, const double* w, 
             if constexpr (NV > 0 && MOPS_PAIR_BARRIER) __builtin_amdgcn_sched_barrier(0);
         }
     }
+    MOPS_MARK(310 + NV);
 }
 
 // Layer + values for one field.  Fast path (fast_ok gave the decreasing
@@ -1070,10 +1094,13 @@ __device__ __forceinline__ bool eval_stream(const Cell<MAXV>& c, int L, int V, c
                                             double pz, double d, int& hint, double& hx, double& hy, double& hz,
                                             double& wv) {
     double w[MAXV];
+    MOPS_MARK(400 + NV);
     if (!weights<MAXV, NV>(c, L, V, px, py, pz, w)) return false;
     Pair S;
+    MOPS_MARK(410 + NV);
     const int layer = layer_eval<MAXV, false, GR, MOPS_HEX_PAIRS ? NV : 0>(c, w, fast_ok<MAXV, NV>(c, c.mono0, weights_finite<MAXV, NV>(c, w), w), f,
                                                   L, d, hint, S);
+    MOPS_MARK(420 + NV);
     if (layer < 0) return false;
     const double zdn = S.zk, zup = S.zm;
     double x = d;
@@ -1088,6 +1115,7 @@ __device__ __forceinline__ bool eval_stream(const Cell<MAXV>& c, int L, int V, c
     hz = S.um2 * t + S.uk2 * (1.0 - t);
     if (sq3(hx, hy, hz) < kNormTiny2) return false;
     wv = t * S.wm + (1.0 - t) * S.wk;
+    MOPS_MARK(430 + NV);
     return true;
 }
 
@@ -1269,7 +1297,13 @@ __global__ void __launch_bounds__(kTrajBlock, (TrajWaves<MAXV, PATH, EULER>::val
     } stamp_end{stamp};
 #endif
     const int64_t pid = a.order ? (int64_t)a.order[slot] : slot;
-    if (a.death[pid] >= 0) return;  // the reference's lambda has returned
+    // Records need no initialisation: the launches from step 0 on write every record of every
+    // particle -- its samples while alive, then (at its death) the zeros the reference's
+    // preallocated trajectory holds (dev::clear_records)
+    if (a.death[pid] >= 0) {  // the reference's lambda has returned
+        if (a.step_begin == 0) dev::clear_records(a.rec, a.rec_stride, pid, 0, a.K);
+        return;
+    }
     double x = a.px[pid], y = a.py[pid], z = a.pz[pid];
     float dep = a.depth[pid];
     int cell = a.cell[pid];
@@ -1286,11 +1320,13 @@ __global__ void __launch_bounds__(kTrajBlock, (TrajWaves<MAXV, PATH, EULER>::val
     // next recording step (the smallest j >= step_begin with (j+1) % rec_period == 0) and its
     // record index, advanced by counting instead of a 64-bit modulo per step
     int64_t rec_next = -1, rec_k = 0;
+    bool rec0 = a.step_begin > 0;  // record 0's step-0 part (seed position, zero velocity) written
     if (a.rec_period > 0) {
         rec_k = a.step_begin / a.rec_period;
         rec_next = (rec_k + 1) * a.rec_period - 1;
     }
     for (int64_t step = a.step_begin; step < a.step_end; ++step) {
+        MOPS_MARK(100);
         if (step == 0) {  // first_loop (:892-901)
             if (cell < 0 || cell >= C) { died = 0; break; }
             dev::load_cell<MAXV, kRC, kNrm>(c, cell, a.cellrec, a.vxyz, a.mono0, a.mono1, a.cxyz, a.cellB);
@@ -1298,6 +1334,10 @@ __global__ void __launch_bounds__(kTrajBlock, (TrajWaves<MAXV, PATH, EULER>::val
             r0[0 * a.rec_stride + pid] = x;
             r0[1 * a.rec_stride + pid] = y;
             r0[2 * a.rec_stride + pid] = z;
+            r0[3 * a.rec_stride + pid] = 0.0;  // (first_vel below, once step 0 evaluates)
+            r0[4 * a.rec_stride + pid] = 0.0;
+            r0[5 * a.rec_stride + pid] = 0.0;
+            rec0 = true;
         } else {  // one-hop nearest-centre walk (:902-922)
             if (cell < 0 || cell >= C) { died = (int)step; break; }
             if (c.id != cell) dev::load_cell<MAXV, kRC, kNrm>(c, cell, a.cellrec, a.vxyz, a.mono0, a.mono1, a.cxyz, a.cellB);
@@ -1332,6 +1372,7 @@ __global__ void __launch_bounds__(kTrajBlock, (TrajWaves<MAXV, PATH, EULER>::val
             }
 #endif
         }
+        MOPS_MARK(110);
         const double d = -1.0 * (double)dep;
         const double r = dev::len3(x, y, z);
         const bool hex = MOPS_HEX && __all(c.nv == 6);  // wave-uniform (dev::eval_at)
@@ -1341,6 +1382,7 @@ __global__ void __launch_bounds__(kTrajBlock, (TrajWaves<MAXV, PATH, EULER>::val
         if (EULER) {
             bool ok = dev::eval_at<MAXV, PATH, PairGroup<PATH, EULER>::value>(hex, c, a.L, a.V, a.f0, a.f1, x, y, z, d, alpha, hint0, hint1, hx, hy, hz, wv);
             if (!ok) { died = (int)step; break; }
+            MOPS_MARK(120);
             const double ax = y * hz - z * hy, ay = z * hx - x * hz, az = x * hy - y * hx;
             const double speed = dev::len3(hx, hy, hz);
             const double th = (speed * a.delta_t) / dev::dmax(1e-12, r);
@@ -1376,6 +1418,7 @@ __global__ void __launch_bounds__(kTrajBlock, (TrajWaves<MAXV, PATH, EULER>::val
             }
             else { nx = x; ny = y; nz = z; }
         }
+        MOPS_MARK(130);
         // vertical update (:977-986)
         const double old_depth = (double)dep;
         double nd = old_depth - wv * (double)a.delta_t;
@@ -1387,6 +1430,7 @@ __global__ void __launch_bounds__(kTrajBlock, (TrajWaves<MAXV, PATH, EULER>::val
             dev::xdiv_norm3(nx, ny, nz, nl, nx, ny, nz);
             nx *= r_new; ny *= r_new; nz *= r_new;
         }
+        MOPS_MARK(140);
         if (step == 0) {  // first_vel (:988-991)
             a.rec[3 * a.rec_stride + pid] = hx;
             a.rec[4 * a.rec_stride + pid] = hy;
@@ -1397,6 +1441,7 @@ __global__ void __launch_bounds__(kTrajBlock, (TrajWaves<MAXV, PATH, EULER>::val
             const int64_t k = rec_k;
             rec_next += a.rec_period;
             ++rec_k;
+            MOPS_MARK(150);
             if (k < a.K) {
                 double* rk = a.rec + k * 6 * a.rec_stride;
                 rk[0 * a.rec_stride + pid] = x;
@@ -1412,6 +1457,9 @@ __global__ void __launch_bounds__(kTrajBlock, (TrajWaves<MAXV, PATH, EULER>::val
     a.depth[pid] = dep;
     a.cell[pid] = cell;
     if (died >= 0) a.death[pid] = died;
+    // slots never sampled: after a death, and past the last record step of a run whose
+    // record period does not fill all K slots (streamline recordT % deltaT != 0)
+    if (died >= 0 || a.step_end == a.n_steps) dev::clear_records(a.rec, a.rec_stride, pid, (rec_k == 0 && rec0) ? 1 : rec_k, a.K);
 }
 
 // exact math helpers against the library (mops_selftest_math)
@@ -2278,9 +2326,10 @@ __device__ __forceinline__ uint64_t spread3(uint64_t v) {  // 21 bits -> every t
     return v;
 }
 
-__global__ void cell_key_kernel(int64_t C, const double4* cxyz, uint64_t* key) {
+__global__ void cell_key_kernel(int64_t C, const double4* cxyz, uint64_t* key, int* ids) {
     const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= C) return;
+    ids[i] = (int)i;
     const double4 p = cxyz[i];
     const double r = sqrt(p.x * p.x + p.y * p.y + p.z * p.z);
     const double s = (r > 0.0) ? 1.0 / r : 0.0;
@@ -2291,17 +2340,32 @@ __global__ void cell_key_kernel(int64_t C, const double4* cxyz, uint64_t* key) {
     key[i] = (spread3(qx) << 2) | (spread3(qy) << 1) | spread3(qz);
 }
 
-// Morton key of each particle's cell; a dead particle (death >= 0, when given) or one without a
-// cell sorts last (~0), so live particles fill whole waves and all-dead waves exit at once
+// rank[c] = position of cell c in the Morton order of the cell centres (ties by cell id)
+__global__ void cell_rank_kernel(int64_t C, const int* sorted_ids, uint32_t* rank) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < C) rank[sorted_ids[i]] = (uint32_t)i;
+}
+
+// Sort bits of a particle key: ranks are < C and the "last" key is C itself
+inline int particle_key_bits(int64_t C) {
+    int b = 1;
+    while (b < 31 && ((int64_t)1 << b) <= C) ++b;
+    return b;
+}
+
+// Morton rank of each particle's cell; a dead particle (death >= 0, when given) or one without a
+// cell sorts last (key C), so live particles fill whole waves and all-dead waves exit at once.
+// 32-bit keys over particle_key_bits(C) bits: 3 radix passes at C ~ 2.4e5 instead of 8 over a
+// 64-bit Morton key.
 __global__ void particle_key_kernel(int64_t n, int64_t C, const int* cell, const int* death,
-                                    const uint64_t* cell_key, uint64_t* key, int* idx, int* n_live) {
+                                    const uint32_t* cell_rank, uint32_t* key, int* idx, int* n_live) {
     const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     bool sorts_first = false;
     if (i < n) {
         const int c = cell[i];
         const bool live = !death || death[i] < 0;
         sorts_first = live && c >= 0 && c < C;
-        key[i] = sorts_first ? cell_key[c] : ~0ULL;
+        key[i] = sorts_first ? cell_rank[c] : (uint32_t)C;
         idx[i] = (int)i;
     }
     if (n_live) {  // one atomic per wave: the particles that sort before the ~0 keys
@@ -2390,7 +2454,7 @@ void free_mesh(mops_mesh* m) {
     if (!m) return;
     (void)hipFree(m->d_cellrec); (void)hipFree(m->d_cxyz); (void)hipFree(m->d_vxyz); (void)hipFree(m->d_cov);
     (void)hipFree(m->d_bary);
-    (void)hipFree(m->d_bkeys); (void)hipFree(m->d_bcells); (void)hipFree(m->d_hkeys); (void)hipFree(m->d_hval); (void)hipFree(m->d_cell_key); (void)hipFree(m->d_cellB); (void)hipFree(m->d_rloc2); (void)hipFree(m->d_ring);
+    (void)hipFree(m->d_bkeys); (void)hipFree(m->d_bcells); (void)hipFree(m->d_hkeys); (void)hipFree(m->d_hval); (void)hipFree(m->d_cell_rank); (void)hipFree(m->d_cellB); (void)hipFree(m->d_rloc2); (void)hipFree(m->d_ring);
     (void)hipFree(m->d_scratch);
     (void)hipFree(m->d_eoc); (void)hipFree(m->d_coe); (void)hipFree(m->d_exyz); (void)hipFree(m->d_rbf_coef);
     (void)hipFree(m->d_rbf_slot);
@@ -2644,8 +2708,29 @@ mops_status mops_mesh_create(const mops_mesh_desc* desc, void* stream, mops_mesh
     if (e == hipSuccess) e = hipStreamSynchronize(s);
     (void)hipFree(tmp); (void)hipFree(keys_in); (void)hipFree(ids_in);
     if (e != hipSuccess) { free_mesh(m); return fail(MOPS_ERR_HIP, std::string("bucket sort: ") + hipGetErrorString(e)); }
-    if ((st = dmalloc(&m->d_cell_key, (size_t)C, &acc)) != MOPS_OK) { free_mesh(m); return st; }
-    cell_key_kernel<<<grid_for(C), kBlock, 0, s>>>(C, m->d_cxyz, m->d_cell_key);
+    {   // Morton rank of every cell (the particles' locality key): one sort of the centres' keys
+        uint64_t *ck = nullptr, *ck_sorted = nullptr;
+        int *cid = nullptr, *cid_sorted = nullptr;
+        void* ctmp = nullptr;
+        size_t ctmp_bytes = 0;
+        e = hipcub::DeviceRadixSort::SortPairs(nullptr, ctmp_bytes, ck, ck_sorted, cid, cid_sorted, (int)C, 0, 63, s);
+        if (e == hipSuccess) e = hipMalloc(&ck, (size_t)C * sizeof(uint64_t));
+        if (e == hipSuccess) e = hipMalloc(&ck_sorted, (size_t)C * sizeof(uint64_t));
+        if (e == hipSuccess) e = hipMalloc(&cid, (size_t)C * sizeof(int));
+        if (e == hipSuccess) e = hipMalloc(&cid_sorted, (size_t)C * sizeof(int));
+        if (e == hipSuccess) e = hipMalloc(&ctmp, std::max<size_t>(ctmp_bytes, 1));
+        if (e == hipSuccess && (st = dmalloc(&m->d_cell_rank, (size_t)C, &acc)) != MOPS_OK) e = hipErrorOutOfMemory;
+        if (e == hipSuccess) {
+            cell_key_kernel<<<grid_for(C), kBlock, 0, s>>>(C, m->d_cxyz, ck, cid);
+            e = hipcub::DeviceRadixSort::SortPairs(ctmp, ctmp_bytes, ck, ck_sorted, cid, cid_sorted, (int)C, 0, 63, s);
+        }
+        if (e == hipSuccess) {
+            cell_rank_kernel<<<grid_for(C), kBlock, 0, s>>>(C, cid_sorted, m->d_cell_rank);
+            e = hipStreamSynchronize(s);
+        }
+        (void)hipFree(ck); (void)hipFree(ck_sorted); (void)hipFree(cid); (void)hipFree(cid_sorted); (void)hipFree(ctmp);
+        if (e != hipSuccess) { free_mesh(m); return fail(MOPS_ERR_HIP, std::string("cell rank sort: ") + hipGetErrorString(e)); }
+    }
     if ((st = dmalloc(&m->d_rloc2, (size_t)C, &acc)) != MOPS_OK) { free_mesh(m); return st; }
     if ((st = dmalloc(&m->d_ring, (size_t)C, &acc)) != MOPS_OK) { free_mesh(m); return st; }
     {   // bucket directory (BucketDir): H = 2^k >= 2 C slots, so it is at most half full
@@ -2984,45 +3069,61 @@ mops_status mops_locate_cells_hinted(const mops_mesh* mesh, int64_t n, const dou
     return MOPS_OK;
 }
 
+// Scratch of the particle locality sort, 256-B aligned parts: keys in, keys out, slot index in,
+// then hipcub's radix temp (sized for all 32 key bits, which covers any particle_key_bits)
+struct OrderScratch {
+    size_t a4 = 0, tmp_bytes = 0, need = 0;
+};
+static hipError_t order_scratch_layout(int64_t n, OrderScratch& o) {
+    hipError_t e = hipcub::DeviceRadixSort::SortPairs(nullptr, o.tmp_bytes, (const uint32_t*)nullptr,
+                                                      (uint32_t*)nullptr, (const int*)nullptr, (int*)nullptr, (int)n,
+                                                      0, 32, (hipStream_t)0);
+    o.a4 = ((size_t)n * 4 + 255) / 256 * 256;
+    o.need = 3 * o.a4 + o.tmp_bytes + 256;  // (+ alignment slack for a caller's buffer)
+    return e;
+}
+static mops_status order_sort(const mops_mesh* mesh, int64_t n, const int32_t* d_cell, const int32_t* d_death,
+                              int32_t* d_order, int32_t* d_n_live, void* scratch, const OrderScratch& o,
+                              hipStream_t s) {
+    char* base = (char*)(((uintptr_t)scratch + 255) / 256 * 256);
+    uint32_t* kin = (uint32_t*)base;
+    uint32_t* kout = (uint32_t*)(base + o.a4);
+    int* vin = (int*)(base + 2 * o.a4);
+    void* tmp = base + 3 * o.a4;
+    if (d_n_live) HIP_TRY(hipMemsetAsync(d_n_live, 0, sizeof(int32_t), s));
+    particle_key_kernel<<<grid_for(n), kBlock, 0, s>>>(n, mesh->C, d_cell, d_death, mesh->d_cell_rank, kin, vin,
+                                                       d_n_live);
+    HIP_TRY(hipGetLastError());
+    size_t tb = o.tmp_bytes;
+    HIP_TRY(hipcub::DeviceRadixSort::SortPairs(tmp, tb, kin, kout, vin, d_order, (int)n, 0,
+                                               particle_key_bits(mesh->C), s));
+    return MOPS_OK;
+}
+
 mops_status mops_order_particles(const mops_mesh* mesh, int64_t n, const int32_t* d_cell, int32_t* d_order,
                                  void* stream) {
     if (!mesh || n < 0 || (n > 0 && (!d_cell || !d_order)) || n >= INT32_MAX)
         return fail(MOPS_ERR_INVALID, "mops_order_particles: invalid argument");
     if (n == 0) return MOPS_OK;
     hipStream_t s = (hipStream_t)stream;
-    size_t tmp_bytes = 0;
-    HIP_TRY(hipcub::DeviceRadixSort::SortPairs(nullptr, tmp_bytes, (const uint64_t*)nullptr, (uint64_t*)nullptr,
-                                               (const int*)nullptr, (int*)nullptr, (int)n, 0, 64, s));
-    const size_t a8 = ((size_t)n * 8 + 255) / 256 * 256, a4 = ((size_t)n * 4 + 255) / 256 * 256;
-    const size_t need = 2 * a8 + a4 + tmp_bytes + 256;
-    if (mesh->scratch_bytes < need) {
+    OrderScratch o;
+    HIP_TRY(order_scratch_layout(n, o));
+    if (mesh->scratch_bytes < o.need) {
         HIP_TRY(hipStreamSynchronize(s));
         (void)hipFree(mesh->d_scratch);
         mesh->d_scratch = nullptr;
         mesh->scratch_bytes = 0;
-        HIP_TRY(hipMalloc(&mesh->d_scratch, need));
-        mesh->scratch_bytes = need;
+        HIP_TRY(hipMalloc(&mesh->d_scratch, o.need));
+        mesh->scratch_bytes = o.need;
     }
-    char* base = (char*)mesh->d_scratch;
-    uint64_t* kin = (uint64_t*)base;
-    uint64_t* kout = (uint64_t*)(base + a8);
-    int* vin = (int*)(base + 2 * a8);
-    void* tmp = base + 2 * a8 + a4;
-    particle_key_kernel<<<grid_for(n), kBlock, 0, s>>>(n, mesh->C, d_cell, nullptr, mesh->d_cell_key, kin, vin, nullptr);
-    HIP_TRY(hipGetLastError());
-    HIP_TRY(hipcub::DeviceRadixSort::SortPairs(tmp, tmp_bytes, kin, kout, vin, d_order, (int)n, 0, 64, s));
-    return MOPS_OK;
+    return order_sort(mesh, n, d_cell, nullptr, d_order, nullptr, mesh->d_scratch, o, s);
 }
 
 int64_t mops_order_scratch_bytes(int64_t n) {
     if (n <= 0 || n >= INT32_MAX) return 0;
-    size_t tmp_bytes = 0;
-    if (hipcub::DeviceRadixSort::SortPairs(nullptr, tmp_bytes, (const uint64_t*)nullptr, (uint64_t*)nullptr,
-                                           (const int*)nullptr, (int*)nullptr, (int)n, 0, 64, (hipStream_t)0) !=
-        hipSuccess)
-        return 0;
-    const size_t a8 = ((size_t)n * 8 + 255) / 256 * 256, a4 = ((size_t)n * 4 + 255) / 256 * 256;
-    return (int64_t)(2 * a8 + a4 + tmp_bytes + 256);
+    OrderScratch o;
+    if (order_scratch_layout(n, o) != hipSuccess) return 0;
+    return (int64_t)o.need;
 }
 
 mops_status mops_permute_arrays(int64_t n, const int32_t* d_order, int32_t count, const mops_perm_array* arrays,
@@ -3062,23 +3163,34 @@ mops_status mops_order_particles_live(const mops_mesh* mesh, int64_t n, const in
         if (d_n_live) HIP_TRY(hipMemsetAsync(d_n_live, 0, sizeof(int32_t), (hipStream_t)stream));
         return MOPS_OK;
     }
-    const int64_t need = mops_order_scratch_bytes(n);
-    if (need <= 0 || scratch_bytes < need)
+    OrderScratch o;
+    HIP_TRY(order_scratch_layout(n, o));
+    if (scratch_bytes < (int64_t)o.need)
         return fail(MOPS_ERR_INVALID, "mops_order_particles_live: scratch smaller than mops_order_scratch_bytes(n)");
-    hipStream_t s = (hipStream_t)stream;
-    size_t tmp_bytes = 0;
-    HIP_TRY(hipcub::DeviceRadixSort::SortPairs(nullptr, tmp_bytes, (const uint64_t*)nullptr, (uint64_t*)nullptr,
-                                               (const int*)nullptr, (int*)nullptr, (int)n, 0, 64, s));
-    const size_t a8 = ((size_t)n * 8 + 255) / 256 * 256, a4 = ((size_t)n * 4 + 255) / 256 * 256;
-    char* base = (char*)(((uintptr_t)d_scratch + 255) / 256 * 256);  // the 256-B slack in the size covers this
-    uint64_t* kin = (uint64_t*)base;
-    uint64_t* kout = (uint64_t*)(base + a8);
-    int* vin = (int*)(base + 2 * a8);
-    void* tmp = base + 2 * a8 + a4;
-    if (d_n_live) HIP_TRY(hipMemsetAsync(d_n_live, 0, sizeof(int32_t), s));
-    particle_key_kernel<<<grid_for(n), kBlock, 0, s>>>(n, mesh->C, d_cell, d_death, mesh->d_cell_key, kin, vin, d_n_live);
+    return order_sort(mesh, n, d_cell, d_death, d_order, d_n_live, d_scratch, o, (hipStream_t)stream);
+}
+
+// records[k][c][i] = 0 for k in [k0, K), slots i in [*n_live, n): blockIdx.y strides over the
+// (k, c) rows, blocks wholly before the live count exit at once
+__global__ void __launch_bounds__(256) records_clear_dead_kernel(int64_t n, const int32_t* __restrict__ n_live,
+                                                                 int64_t k0, int64_t rows, double* __restrict__ rec,
+                                                                 int64_t stride) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const int64_t nl = *n_live;
+    if ((int64_t)(blockIdx.x + 1) * blockDim.x <= nl || i >= n || i < nl) return;
+    for (int64_t r = blockIdx.y; r < rows; r += gridDim.y) rec[(k0 * 6 + r) * stride + i] = 0.0;
+}
+
+mops_status mops_records_clear_dead(int64_t n, const int32_t* d_n_live, int64_t k_begin, int64_t K,
+                                    double* d_records, int64_t record_stride, void* stream) {
+    if (n < 0 || k_begin < 0 || K < 0 || (n > 0 && (!d_n_live || !d_records)) || record_stride < n)
+        return fail(MOPS_ERR_INVALID, "mops_records_clear_dead: invalid argument");
+    if (n == 0 || k_begin >= K) return MOPS_OK;
+    const int64_t rows = (K - k_begin) * 6;
+    const dim3 grid((unsigned)((n + 255) / 256), (unsigned)(rows < 1024 ? rows : 1024));
+    records_clear_dead_kernel<<<grid, 256, 0, (hipStream_t)stream>>>(n, d_n_live, k_begin, rows, d_records,
+                                                                     record_stride);
     HIP_TRY(hipGetLastError());
-    HIP_TRY(hipcub::DeviceRadixSort::SortPairs(tmp, tmp_bytes, kin, kout, vin, d_order, (int)n, 0, 64, s));
     return MOPS_OK;
 }
 
@@ -3252,8 +3364,8 @@ mops_status mops_run_trajectories(const mops_mesh* mesh, const mops_field* front
         if ((st = dmalloc(&tmp, (size_t)(n * P), nullptr)) != MOPS_OK) break;
         if ((st = dmalloc(&sal, (size_t)(n * P), nullptr)) != MOPS_OK) break;
         if ((st = dmalloc(&last, (size_t)(n * 3), nullptr)) != MOPS_OK) break;
-        hipError_t e = hipMemsetAsync(rec, 0, (size_t)(K * 6 * n) * sizeof(double), s);
-        if (e == hipSuccess) e = hipMemsetAsync(death, 0xff, (size_t)n * sizeof(int), s);  // -1 = alive
+        // (rec needs no clearing: the launch from step 0 writes every record slot)
+        hipError_t e = hipMemsetAsync(death, 0xff, (size_t)n * sizeof(int), s);  // -1 = alive
         if (e != hipSuccess) { st = fail(MOPS_ERR_HIP, hipGetErrorString(e)); break; }
         // default_cell_id: entries < 0 are located (MPASOVisualizerKernels.cpp:683-690)
         std::vector<int32_t> hc((size_t)n, -1);

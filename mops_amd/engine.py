@@ -336,8 +336,6 @@ class ParticleSet:
                 cur = getattr(self, k)
                 setattr(self, k, self._spare[k])
                 self._spare[k] = cur
-            if record_slots > 0 and record_slots < self.records.shape[0]:
-                self.records[record_slots:].zero_()  # (the spare slab's unwritten slots must be zero)
         else:
             back = (L.PermArray * len(names))(*[desc(self._spare[k], getattr(self, k), k, e) for k, e in names])
             L.check(lib.mops_permute_arrays(n, None, len(names), back, _stream_handle(s)), "mops_permute_arrays")
@@ -353,9 +351,11 @@ class ParticleSet:
         live particles in the Morton order of their current cell first, dead ones after them, so
         the next launches run full waves of live lanes and all-dead waves exit at once.  The SoA
         state, seeds, slot ids and the first ``records_written`` record slots are permuted with
-        them (later slots are still all zero); results are unchanged (every particle is
-        independent, finalize writes each slot's line at its id).  Re-entrant across disjoint
-        ranges on different streams (each range has its own scratch)."""
+        them; the dead particles' later slots are cleared again where they land
+        (mops_records_clear_dead: they hold no samples, the live particles' ones are written by
+        the next launches).  Results are unchanged (every particle is independent, finalize
+        writes each slot's line at its id).  Re-entrant across disjoint ranges on different
+        streams (each range has its own scratch)."""
         torch = self.torch
         n = hi - lo
         if n <= 1:
@@ -380,19 +380,22 @@ class ParticleSet:
                                               C.c_void_p(self._n_live[key].data_ptr()),
                                               C.c_void_p(scratch.data_ptr()), scratch.numel(), _stream_handle(s)),
                 "mops_order_particles_live")
-        self._apply_order(self.order, lo, hi, s, min(int(records_written), self.records.shape[0]))
+        kw = min(int(records_written), self.records.shape[0])
+        self._apply_order(self.order, lo, hi, s, kw)
+        L.check(lib.mops_records_clear_dead(n, C.c_void_p(self._n_live[key].data_ptr()), kw, self.records.shape[0],
+                                            C.c_void_p(self.records.data_ptr() + 8 * lo), self.n,
+                                            _stream_handle(s)), "mops_records_clear_dead")
 
     def reset(self, depth=None):
         self.x.copy_(self.seeds[:, 0]); self.y.copy_(self.seeds[:, 1]); self.z.copy_(self.seeds[:, 2])
         if depth is not None:
             self.depth.fill_(float(depth))
         self.death.fill_(-1)
-        self.records.zero_()
-        self._written = False
+        self._written = False  # (records: every slot is rewritten by the launches from step 0)
 
     def reseed(self, seeds, depth, stream=None, hint_cells: bool = False):
         """Start a new run from device-resident seeds [n,3] (f64) and depth (scalar
-        or [n] f32): state <- seeds, death cleared, records zeroed, seed cells
+        or [n] f32): state <- seeds, death cleared (records need no clearing), seed cells
         located (the reference's calcInWhichCells per run) and re-ordered.
         ``hint_cells``: the seeds continue this set's particles (a chained pair),
         so each particle's current cell seeds the exact locate (same answer)."""
@@ -411,7 +414,6 @@ class ParticleSet:
         else:
             self.depth.fill_(float(np.float32(depth)))
         self.death.fill_(-1)
-        self.records.zero_()
         self._written = False
         self.mesh.locate(self.seeds.data_ptr(), self.cell.data_ptr(), self.n, stream=h,
                          d_hint=None if hint is None else hint.data_ptr())
@@ -456,8 +458,7 @@ class ParticleSet:
         last live lane finishes."""
         torch = self.torch
         nparts = max(1, len(streams))
-        waves = -(-self.n // 64)
-        pb = [min(self.n, 64 * (waves * k // nparts)) for k in range(nparts + 1)]
+        pb = self.part_bounds(nparts)
         span = int(step_end) - int(step_begin)
         chunks = max(1, min(int(chunks), span))
         tb = [int(step_begin) + span * k // chunks for k in range(chunks + 1)]
@@ -500,13 +501,23 @@ class ParticleSet:
                     timing.append((e0, e1))
         self._written = True
 
+    def part_bounds(self, nparts: int):
+        """Slot bounds of ``nparts`` contiguous particle parts in whole waves (advance_pipelined)."""
+        nparts = max(1, int(nparts))
+        waves = -(-self.n // 64)
+        return [min(self.n, 64 * (waves * k // nparts)) for k in range(nparts + 1)]
+
     def record_period(self, pathline: bool) -> int:
         import math
         if pathline:
             return int(self.cfg.recordT // self.cfg.deltaT)
         return int(self.cfg.recordT // math.gcd(int(self.cfg.recordT), int(self.cfg.deltaT)))
 
-    def finalize(self, pathline: bool, stream=None):
+    def finalize(self, pathline: bool, stream=None, streams=None, timing=None):
+        """Lines of every particle in seed order (mops_traj_finalize).  ``streams``: the
+        advance_pipelined part streams -- each part's lines are assembled on its own stream right
+        after its last chunk, so one part's assembly overlaps the other parts' final waves (the
+        caller joins the streams afterwards); ``timing`` receives (start, end) events per launch."""
         torch = self.torch
         dev = self.seeds.device
         P = self.K + 1
@@ -515,10 +526,32 @@ class ParticleSet:
         tmp = torch.empty((self.n, P), dtype=torch.float64, device=dev)
         sal = torch.empty_like(tmp)
         last = torch.empty((self.n, 3), dtype=torch.float64, device=dev)
-        st = L.load().mops_traj_finalize(self.n, self.K, C.c_void_p(self.seeds.data_ptr()),
-                                         C.c_void_p(self.records.data_ptr()), self.n, 1 if pathline else 0,
-                                         C.c_void_p(self.ids.data_ptr()), C.c_void_p(pts.data_ptr()), C.c_void_p(vel.data_ptr()),
-                                         C.c_void_p(tmp.data_ptr()), C.c_void_p(sal.data_ptr()),
-                                         C.c_void_p(last.data_ptr()), _stream_handle(stream))
-        L.check(st, "mops_traj_finalize")
+        outs = (pts, vel, tmp, sal, last)
+        if streams:
+            pb = self.part_bounds(len(streams))
+            parts = [(pb[k], pb[k + 1], streams[k]) for k in range(len(streams))]
+            for t in outs:  # written on the part streams: the allocator must wait for them
+                for st in streams:
+                    t.record_stream(st if isinstance(st, torch.cuda.Stream) else torch.cuda.ExternalStream(int(st)))
+        else:
+            parts = [(0, self.n, stream)]
+        lib = L.load()
+        for lo, hi, st in parts:
+            if hi <= lo:
+                continue
+            if timing is not None:
+                e0 = torch.cuda.Event(enable_timing=True); e1 = torch.cuda.Event(enable_timing=True)
+                ts = st if isinstance(st, torch.cuda.Stream) else (
+                    torch.cuda.ExternalStream(int(st)) if st else torch.cuda.default_stream(dev))
+                e0.record(ts)
+            # a part's slots write the lines ids[slot] of the full outputs
+            rc = lib.mops_traj_finalize(hi - lo, self.K, C.c_void_p(self.seeds.data_ptr() + 24 * lo),
+                                        C.c_void_p(self.records.data_ptr() + 8 * lo), self.n, 1 if pathline else 0,
+                                        C.c_void_p(self.ids.data_ptr() + 4 * lo), C.c_void_p(pts.data_ptr()),
+                                        C.c_void_p(vel.data_ptr()), C.c_void_p(tmp.data_ptr()),
+                                        C.c_void_p(sal.data_ptr()), C.c_void_p(last.data_ptr()), _stream_handle(st))
+            L.check(rc, "mops_traj_finalize")
+            if timing is not None:
+                e1.record(ts)
+                timing.append((e0, e1))
         return dict(points=pts, velocity=vel, temperature=tmp, salinity=sal, lastPoint=last)

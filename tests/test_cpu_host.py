@@ -73,7 +73,7 @@ def test_abi_exports_every_header_symbol(engine_lib):
 def test_abi_host_only_calls(engine_lib):
     import ctypes as C
     from mops_amd import _lib
-    assert engine_lib.mops_abi_version() == 3
+    assert engine_lib.mops_abi_version() == 4
     cfg = _lib.TrajCfg(120, 86400, 3600, 0, 1)
     assert engine_lib.mops_traj_num_records(C.byref(cfg)) == 24
     assert engine_lib.mops_traj_num_steps(C.byref(cfg)) == 720

@@ -293,6 +293,7 @@ def test_dead_particle_compaction_is_result_invariant(gpu, dev_small, small_case
     a.advance(f0, back, 0, cfg.n_steps)
     la = a.finalize(pathline=back_on)
     b = ParticleSet(dm, seeds, 250.0, cfg)
+    b.records.fill_(float("nan"))  # records need no clearing (every slot is written, zeros at death)
     streams = [torch.cuda.Stream() for _ in range(2)]
     for st in streams:
         st.wait_stream(torch.cuda.current_stream())
@@ -308,6 +309,19 @@ def test_dead_particle_compaction_is_result_invariant(gpu, dev_small, small_case
     death = b.original(b.death).cpu().numpy()
     if method == 0:
         assert (death >= 0).sum() > 50 and (death > 0).any()  # Q1 deaths during the run
+    # a second run of the same set over the first run's records, its lines assembled per part on
+    # the part streams (bench.py's overlapped finalize)
+    c_seeds = torch.as_tensor(seeds, dtype=torch.float64, device=gpu)
+    b.reseed(c_seeds, 250.0)
+    for st in streams:
+        st.wait_stream(torch.cuda.current_stream())
+    b.advance_pipelined(f0, back, 0, cfg.n_steps, streams, 5, compact=True)
+    lc = b.finalize(pathline=back_on, streams=streams)
+    for st in streams:
+        torch.cuda.current_stream().wait_stream(st)
+    torch.cuda.synchronize()
+    for k in ("points", "velocity", "temperature", "salinity", "lastPoint"):
+        assert torch.equal(la[k], lc[k]), k
     # the oracle agrees on a sample (the compaction moved dead particles between waves)
     r0 = oracle_lib.preprocess(mesh, s0)
     r1 = oracle_lib.preprocess(mesh, s1) if back_on else None
