@@ -67,6 +67,9 @@ constexpr int kBlock = 256;
 #endif
 constexpr int kTrajBlock = MOPS_TRAJ_BLOCK;
 constexpr int kPairRec = 10;  // doubles per level-pair record (see mops_field::d_pr)
+#ifndef MOPS_PAIR_TEST
+#define MOPS_PAIR_TEST 1  // the walk's pair test (dev::walk)
+#endif
 #ifndef MOPS_PR_LEVEL_MAJOR
 #define MOPS_PR_LEVEL_MAJOR 1  // record (v, k) at index (k-1)*V + v (level-major; 0: v*(L-1) + k-1, vertex-major)
 #endif
@@ -241,6 +244,22 @@ __device__ __forceinline__ double kconst(unsigned hi, unsigned lo, unsigned salt
 }
 #define MOPS_K(bits) dev::kconst((unsigned)((bits) >> 32), (unsigned)((bits) & 0xffffffffULL), salt)
 
+// a * b + k with k an SGPR-pair constant (MOPS_K), as one VOP3 v_fma_f64: the compiler's own
+// choice is v_fmac_f64, whose tied accumulator needs k copied into a VGPR pair first (two
+// v_mov_b32 per Horner step).  Same operation, same rounding.
+#ifndef MOPS_SINCOS_VOP3
+#define MOPS_SINCOS_VOP3 1
+#endif
+__device__ __forceinline__ double fma_k(double a, double b, double k) {
+#if MOPS_SINCOS_VOP3
+    double r;
+    asm("v_fma_f64 %0, %1, %2, %3" : "=v"(r) : "v"(a), "v"(b), "s"(k));
+    return r;
+#else
+    return __builtin_fma(a, b, k);
+#endif
+}
+
 // sin and cos of |x| < 0.78, bit-identical to the device library's sin(x) / cos(x):
 // their gfx950 expansion reduces x by k = rint(|x| * 2/pi) with a Cody-Waite
 // chain that, for k = 0, returns r = |x| and rr = +0 exactly, evaluates both
@@ -254,20 +273,20 @@ __device__ __forceinline__ void sincos_small(double x, double& s, double& c, uns
     const double h = x2 * 0.5;
     double t16 = __builtin_fma(MOPS_K(0xbda907db46cc5e42ULL), x2, MOPS_K(0x3e21eeb69037ab78ULL));
     const double t12 = 1.0 - h;
-    double t18 = __builtin_fma(x2, t16, MOPS_K(0xbe927e4fa17f65f6ULL));
+    double t18 = fma_k(x2, t16, MOPS_K(0xbe927e4fa17f65f6ULL));
     const double t14 = 1.0 - t12;
-    t16 = __builtin_fma(x2, t18, MOPS_K(0x3efa01a019f4ec90ULL));
+    t16 = fma_k(x2, t18, MOPS_K(0x3efa01a019f4ec90ULL));
     double t10 = t14 - h;
-    t18 = __builtin_fma(x2, t16, MOPS_K(0xbf56c16c16c16967ULL));
+    t18 = fma_k(x2, t16, MOPS_K(0xbf56c16c16c16967ULL));
     const double x4 = x2 * x2;
-    t16 = __builtin_fma(x2, t18, MOPS_K(0x3fa5555555555555ULL));
+    t16 = fma_k(x2, t18, MOPS_K(0x3fa5555555555555ULL));
     t10 = __builtin_fma(r, -rr, t10);
     t10 = __builtin_fma(x4, t16, t10);
     c = t12 + t10;
     double u12 = __builtin_fma(MOPS_K(0x3de5e0b2f9a43bb8ULL), x2, MOPS_K(0xbe5ae600b42fdfa7ULL));
-    double u14 = __builtin_fma(x2, u12, MOPS_K(0x3ec71de3796cde01ULL));
-    u12 = __builtin_fma(x2, u14, MOPS_K(0xbf2a01a019e83e5cULL));
-    u14 = __builtin_fma(x2, u12, MOPS_K(0x3f81111111110bb3ULL));
+    double u14 = fma_k(x2, u12, MOPS_K(0x3ec71de3796cde01ULL));
+    u12 = fma_k(x2, u14, MOPS_K(0xbf2a01a019e83e5cULL));
+    u14 = fma_k(x2, u12, MOPS_K(0x3f81111111110bb3ULL));
     u12 = r * -x2;
     double u16 = rr * 0.5;
     u16 = __builtin_fma(u12, u14, u16);
@@ -448,6 +467,10 @@ struct Cell {
     // lds_n: IsInMesh edge normals n_i = X_i x X_{i+1} (slot pairs as in dev::weights), computed
     // by load_cell into this lane's LDS column: component j of slot i at nrm[(3 * i + j) * kTrajBlock]
     double* nrm;
+    // pair test (dev::walk): the bisector of c and its nearest neighbour at the last anchor, valid
+    // in a second, larger ball around it -- {n.x, n.y, n.z, k, rb2} at pr2[j * kTrajBlock] (LDS);
+    // rb2 < 0 = none (load_cell)
+    double* pr2;
     const double4* __restrict__ vxyz;   // rc == false: polygon re-read per evaluation (L1-resident)
     const double* __restrict__ cellB;   // rc == false: per-cell B_i [C][MAXV] (cell_b_kernel)
 };
@@ -463,6 +486,7 @@ __device__ __forceinline__ void load_cell(Cell<MAXV>& c, int cell, const int* __
         const double4 q = cxyz[cell];
         c.cx = q.x; c.cy = q.y; c.cz = q.z; c.rs2 = q.w;
     }
+    if constexpr (NRM && MOPS_PAIR_TEST) c.pr2[4 * kTrajBlock] = -1.0;  // no pair test before a walk in c
     constexpr int REC = ((1 + 2 * MAXV) + 3) / 4 * 4;
     const int* r = cellrec + (int64_t)cell * REC;
     int buf[REC];
@@ -857,6 +881,20 @@ __device__ __forceinline__ int bracket_mono(const Cell<MAXV>& c, const double* w
 // sets the anchor to the cell centre with rs = (min_nb |c_nb - c|)/2 - 1 m,
 // the same argument at p0 = c.  A walk that changes cell leaves the anchor of
 // the new cell's load_cell.
+//
+// Pair test (MOPS_PAIR_TEST).  Near an edge of c the stay ball is small (g is the gap to the
+// neighbour across that edge), so a particle drifting along the edge walked every few steps --
+// the walk's gathers and their dependent round trips cost ~14% of a config-2 step (measured by
+// running every walk twice).  The walk that keeps c therefore also records, for its anchor p0, the
+// gap g2 of the second-nearest distinct neighbour and the bisector of c and the nearest one, nb1:
+// f(p) = |p - c1|^2 - |p - c|^2 = n.p + k, n = 2 (c - c1), k = |c1|^2 - |c|^2.  Inside the ball
+// |p - p0| < (g2 - 0.01 m) / 2 every neighbour but nb1 stays farther than c by more than rounding
+// (same argument as above), so the reference's argmin is c or nb1; and there d_1 + d_c <= D =
+// 2 rb + d_c(p0) + d_1(p0), so f(p) > 0.01 D means d_1 - d_c > 0.01 m, far above the < 1e-7 m
+// error of a computed distance, i.e. c stays the unique minimum.  The computed f errs by < 1e-13
+// (|c|^2 + |c1|^2 + |p0|^2 + rb^2) (a few hundred ulps of the largest term, over-estimated by
+// ~50x), which is subtracted from k with the 0.01 D margin.  The caller then keeps c without
+// walking; any other outcome walks.  (MOPS_PAIR_TEST, defined with the other build switches.)
 #if defined(MOPS_PROF)
 // Event counters for perf experiments (tools/build_variant.sh -DMOPS_PROF), read back with
 // mops_debug_prof: [0] lane-steps, [1] lane walks, [2] lane cell loads, [3] wave-steps,
@@ -864,7 +902,7 @@ __device__ __forceinline__ int bracket_mono(const Cell<MAXV>& c, const double* w
 __device__ unsigned long long g_prof[8];
 #endif
 
-template <int MAXV>
+template <int MAXV, bool PAIR>
 __device__ __forceinline__ int walk(Cell<MAXV>& c, int cell, double x, double y, double z,
                                     const int* __restrict__ cellrec, const double4* __restrict__ cxyz, int C) {
     MOPS_CNT(4, 1);
@@ -910,15 +948,39 @@ __device__ __forceinline__ int walk(Cell<MAXV>& c, int cell, double x, double y,
     }
     // c attains the minimum and no neighbour ties it (so every finite s_k > s_c)
     double s2 = inf;
+    int id1 = -1;  // the nearest neighbour (first of equals)
 #pragma unroll
     for (int k = 0; k < MAXV; ++k)
-        if (ok[k] && s[k] < s2) s2 = s[k];
+        if (ok[k] && s[k] < s2) { s2 = s[k]; id1 = id[k]; }
+    double rb2 = -1.0;
     if (!(s2 < inf)) {
         c.rs2 = inf;  // no neighbour with a finite distance: the walk can only keep c
     } else {
-        const double ra = (sqrt(s2) - sqrt(sc) - 0.01) * 0.5;
+        const double dc = sqrt(sc), d1 = sqrt(s2);
+        const double ra = (d1 - dc - 0.01) * 0.5;
         c.rs2 = (ra > 0.0) ? ra * ra * (1.0 - 1e-9) : -1.0;
+        if constexpr (PAIR) {
+            double s3 = inf;  // the second-nearest distinct neighbour
+#pragma unroll
+            for (int k = 0; k < MAXV; ++k)
+                if (ok[k] && id[k] != id1 && s[k] < s3) s3 = s[k];
+            const double rb = (s3 < inf) ? (sqrt(s3) - dc - 0.01) * 0.5 : -1.0;
+            if (ra > 0.0 && rb > ra) {
+                const double4 q1 = cxyz[id1];
+                const double c2 = qc.x * qc.x + qc.y * qc.y + qc.z * qc.z;
+                const double c12 = q1.x * q1.x + q1.y * q1.y + q1.z * q1.z;
+                const double p2 = x * x + y * y + z * z;
+                const double D = 2.0 * rb + dc + d1;
+                const double err = 1e-13 * (c2 + c12 + p2 + rb * rb);
+                c.pr2[0 * kTrajBlock] = 2.0 * (qc.x - q1.x);
+                c.pr2[1 * kTrajBlock] = 2.0 * (qc.y - q1.y);
+                c.pr2[2 * kTrajBlock] = 2.0 * (qc.z - q1.z);
+                c.pr2[3 * kTrajBlock] = (c12 - c2) - 0.01 * D - err;
+                rb2 = rb * rb * (1.0 - 1e-9);
+            }
+        }
     }
+    if constexpr (PAIR) c.pr2[4 * kTrajBlock] = rb2;
     c.cx = x; c.cy = y; c.cz = z;
     return cell;
 }
@@ -1316,6 +1378,9 @@ __global__ void __launch_bounds__(kTrajBlock, (TrajWaves<MAXV, PATH, EULER>::val
     constexpr bool kRC = RCache<MAXV, PATH, EULER>::value, kNrm = LdsNormals<MAXV, PATH, EULER>::value;
     __shared__ double s_nrm[kNrm ? 3 * MAXV * kTrajBlock : 1];  // per-lane edge normals (Cell::nrm)
     c.nrm = s_nrm + threadIdx.x;
+    constexpr bool kPairT = kNrm && MOPS_PAIR_TEST;  // (load_cell resets it with the normals)
+    __shared__ double s_pr2[kPairT ? 5 * kTrajBlock : 1];  // per-lane pair test (Cell::pr2, dev::walk)
+    c.pr2 = s_pr2 + threadIdx.x;
     const int C = a.C;
     // next recording step (the smallest j >= step_begin with (j+1) % rec_period == 0) and its
     // record index, advanced by counting instead of a 64-bit modulo per step
@@ -1346,10 +1411,17 @@ __global__ void __launch_bounds__(kTrajBlock, (TrajWaves<MAXV, PATH, EULER>::val
             // the reference's argmin (c listed last, strict <) keeps c (dev::walk).
             const double ex = x - c.cx, ey = y - c.cy, ez = z - c.cz;
 #if defined(MOPS_PROF)
-            const bool walking = !(ex * ex + ey * ey + ez * ez < c.rs2);
+            const double e2p = ex * ex + ey * ey + ez * ez;
+            bool stay_p = e2p < c.rs2;
+            if constexpr (kPairT) {
+                if (!stay_p && e2p < c.pr2[4 * kTrajBlock])
+                    stay_p = c.pr2[0] * x + c.pr2[kTrajBlock] * y + c.pr2[2 * kTrajBlock] * z +
+                             c.pr2[3 * kTrajBlock] > 0.0;
+            }
+            const bool walking = !stay_p;
             bool loading = false;
             if (walking) {
-                cell = dev::walk<MAXV>(c, cell, x, y, z, a.cellrec, a.cxyz, C);
+                cell = dev::walk<MAXV, kPairT>(c, cell, x, y, z, a.cellrec, a.cxyz, C);
                 loading = c.id != cell;
                 if (c.id != cell) dev::load_cell<MAXV, kRC, kNrm>(c, cell, a.cellrec, a.vxyz, a.mono0, a.mono1, a.cxyz, a.cellB);
             }
@@ -1365,8 +1437,26 @@ __global__ void __launch_bounds__(kTrajBlock, (TrajWaves<MAXV, PATH, EULER>::val
                 }
             }
 #else
-            if (!(ex * ex + ey * ey + ez * ez < c.rs2)) {
-                cell = dev::walk<MAXV>(c, cell, x, y, z, a.cellrec, a.cxyz, C);
+            const double e2 = ex * ex + ey * ey + ez * ez;
+            bool stay = e2 < c.rs2;
+            if constexpr (kPairT) {
+                if (!stay && e2 < c.pr2[4 * kTrajBlock])  // second ball: only nb1 competes (dev::walk)
+                    stay = c.pr2[0] * x + c.pr2[kTrajBlock] * y + c.pr2[2 * kTrajBlock] * z +
+                           c.pr2[3 * kTrajBlock] > 0.0;
+            }
+#if defined(MOPS_ABL_NOWALK)  // ablation: never walk (wrong results; the walks' cost bound)
+            if (false) {
+#else
+            if (!stay) {
+#endif
+#if defined(MOPS_ABL_WALK2)  // ablation: every walk runs twice (same result; one walk's cost)
+                {
+                    double xo = x;
+                    asm volatile("" : "+v"(xo));
+                    cell = dev::walk<MAXV, kPairT>(c, cell, xo, y, z, a.cellrec, a.cxyz, C);
+                }
+#endif
+                cell = dev::walk<MAXV, kPairT>(c, cell, x, y, z, a.cellrec, a.cxyz, C);
                 if (c.id != cell) MOPS_CNT(5, 1);
                 if (c.id != cell) dev::load_cell<MAXV, kRC, kNrm>(c, cell, a.cellrec, a.vxyz, a.mono0, a.mono1, a.cxyz, a.cellB);
             }
