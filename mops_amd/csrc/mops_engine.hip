@@ -99,7 +99,9 @@ struct mops_mesh {
     int2* d_hval = nullptr;       // [H]
     uint32_t hmask = 0;           // H - 1
     uint32_t* d_cell_rank = nullptr;  // rank of each cell in the Morton order of the centres (particle locality order)
-    double* d_cellB = nullptr;       // [C][maxv] Wachspress B_i of each cell polygon
+    // [C][maxv] each cell's polygon in rotated slot order with its Wachspress weights' numerators:
+    // slot j = {poly[j-1] (poly[-1] = poly[nv-1]), B_j = area(poly[j-1], poly[j], poly[j+1])}, zeros past nv
+    double4* d_cpoly = nullptr;
     double* d_rloc2 = nullptr;       // [C] squared hinted-locate radius (locate_radius_kernel)
     double* d_ring = nullptr;        // [C] hinted-locate ring distance (locate_radius_kernel)
     // grow-only scratch for mops_order_particles (not re-entrant, like the reference's global app)
@@ -445,6 +447,11 @@ __device__ __forceinline__ double dclamp(double v, double lo, double hi) { retur
 #ifndef MOPS_RC_PR
 #define MOPS_RC_PR 0
 #endif
+// modes without the register polygon: read a slot from the per-cell packed polygon (one 32-B
+// {x, y, z, B_j}, mops_mesh::d_cpoly) rather than the vertex array + B_j (1 = packed)
+#ifndef MOPS_CPOLY
+#define MOPS_CPOLY 1
+#endif
 
 // Per-cell stencil cached in registers while the particle stays in the cell.
 template <int MAXV>
@@ -472,14 +479,14 @@ struct Cell {
     // rb2 < 0 = none (load_cell)
     double* pr2;
     const double4* __restrict__ vxyz;   // rc == false: polygon re-read per evaluation (L1-resident)
-    const double* __restrict__ cellB;   // rc == false: per-cell B_i [C][MAXV] (cell_b_kernel)
+    const double4* __restrict__ cpoly;  // rc == false: per-cell rotated polygon + B_i [C][MAXV] (cell_poly_kernel)
 };
 
 template <int MAXV, bool RC, bool NRM>
 __device__ __forceinline__ void load_cell(Cell<MAXV>& c, int cell, const int* __restrict__ cellrec,
                                           const double4* __restrict__ vxyz, const uint32_t* __restrict__ mono0,
                                           const uint32_t* __restrict__ mono1, const double4* __restrict__ cxyz,
-                                          const double* __restrict__ cellB) {
+                                          const double4* __restrict__ cpoly) {
     c.mono0 = mono0[cell];
     c.mono1 = mono1[cell];
     {
@@ -508,7 +515,7 @@ __device__ __forceinline__ void load_cell(Cell<MAXV>& c, int cell, const int* __
         if (k == nv - 1) c.vlast = c.vid[k];
     if constexpr (!RC) {
         c.vxyz = vxyz;
-        c.cellB = cellB;
+        c.cpoly = cpoly;
     }
     if constexpr (RC || NRM) {
         double px[MAXV], py[MAXV], pz[MAXV];  // natural order
@@ -595,9 +602,15 @@ __device__ __forceinline__ bool weights(const Cell<MAXV>& c, int L, int V, doubl
             X[j] = c.x[j]; Y[j] = c.y[j]; Z[j] = c.z[j]; BB[j] = c.B[j];
         } else {
             if (j < nv) {
+#if MOPS_CPOLY
+                // one 32-B slot {x, y, z, B_j} of the cell's packed polygon: 2 VMEM instead of 3
+                const double4 q = c.cpoly[(int64_t)c.id * MAXV + j];
+                X[j] = q.x; Y[j] = q.y; Z[j] = q.z; BB[j] = q.w;
+#else
                 const double4 q = c.vxyz[j == 0 ? c.vlast : c.vid[(j + MAXV - 1) % MAXV]];
                 X[j] = q.x; Y[j] = q.y; Z[j] = q.z;
-                BB[j] = c.cellB[(int64_t)c.id * MAXV + j];
+                BB[j] = c.cpoly[(int64_t)c.id * MAXV + j].w;
+#endif
             } else {
                 X[j] = 0.0; Y[j] = 0.0; Z[j] = 0.0; BB[j] = 0.0;
             }
@@ -1247,7 +1260,7 @@ struct TrajArgs {
     const uint32_t* __restrict__ mono1;
     const int* __restrict__ order;  // slot -> particle (NULL = identity)
     const int* __restrict__ n_live;  // device count of leading live slots (compaction), NULL = all n
-    const double* __restrict__ cellB;  // per-cell Wachspress B_i
+    const double4* __restrict__ cpoly;  // per-cell rotated polygon + Wachspress B_i (mops_mesh::d_cpoly)
     double* px; double* py; double* pz;
     float* depth;
     int* cell;
@@ -1394,7 +1407,7 @@ __global__ void __launch_bounds__(kTrajBlock, (TrajWaves<MAXV, PATH, EULER>::val
         MOPS_MARK(100);
         if (step == 0) {  // first_loop (:892-901)
             if (cell < 0 || cell >= C) { died = 0; break; }
-            dev::load_cell<MAXV, kRC, kNrm>(c, cell, a.cellrec, a.vxyz, a.mono0, a.mono1, a.cxyz, a.cellB);
+            dev::load_cell<MAXV, kRC, kNrm>(c, cell, a.cellrec, a.vxyz, a.mono0, a.mono1, a.cxyz, a.cpoly);
             double* r0 = a.rec;
             r0[0 * a.rec_stride + pid] = x;
             r0[1 * a.rec_stride + pid] = y;
@@ -1405,7 +1418,7 @@ __global__ void __launch_bounds__(kTrajBlock, (TrajWaves<MAXV, PATH, EULER>::val
             rec0 = true;
         } else {  // one-hop nearest-centre walk (:902-922)
             if (cell < 0 || cell >= C) { died = (int)step; break; }
-            if (c.id != cell) dev::load_cell<MAXV, kRC, kNrm>(c, cell, a.cellrec, a.vxyz, a.mono0, a.mono1, a.cxyz, a.cellB);
+            if (c.id != cell) dev::load_cell<MAXV, kRC, kNrm>(c, cell, a.cellrec, a.vxyz, a.mono0, a.mono1, a.cxyz, a.cpoly);
             // Exact shortcut: inside the stay ball around the anchor every
             // neighbour is strictly farther than c by more than rounding, so
             // the reference's argmin (c listed last, strict <) keeps c (dev::walk).
@@ -1423,7 +1436,7 @@ __global__ void __launch_bounds__(kTrajBlock, (TrajWaves<MAXV, PATH, EULER>::val
             if (walking) {
                 cell = dev::walk<MAXV, kPairT>(c, cell, x, y, z, a.cellrec, a.cxyz, C);
                 loading = c.id != cell;
-                if (c.id != cell) dev::load_cell<MAXV, kRC, kNrm>(c, cell, a.cellrec, a.vxyz, a.mono0, a.mono1, a.cxyz, a.cellB);
+                if (c.id != cell) dev::load_cell<MAXV, kRC, kNrm>(c, cell, a.cellrec, a.vxyz, a.mono0, a.mono1, a.cxyz, a.cpoly);
             }
             {
                 const unsigned long long bw = __ballot(walking), bl = __ballot(loading), ba = __ballot(1);
@@ -1458,7 +1471,7 @@ __global__ void __launch_bounds__(kTrajBlock, (TrajWaves<MAXV, PATH, EULER>::val
 #endif
                 cell = dev::walk<MAXV, kPairT>(c, cell, x, y, z, a.cellrec, a.cxyz, C);
                 if (c.id != cell) MOPS_CNT(5, 1);
-                if (c.id != cell) dev::load_cell<MAXV, kRC, kNrm>(c, cell, a.cellrec, a.vxyz, a.mono0, a.mono1, a.cxyz, a.cellB);
+                if (c.id != cell) dev::load_cell<MAXV, kRC, kNrm>(c, cell, a.cellrec, a.vxyz, a.mono0, a.mono1, a.cxyz, a.cpoly);
             }
 #endif
         }
@@ -2286,10 +2299,13 @@ __global__ void mono_kernel(int64_t C, int maxv, int rec_ints, const int* cellre
     mono[i] = ok ? (0x80000000u | ((uint32_t)km << 20) | zmask) : 0u;
 }
 
-// Wachspress B_i = area(poly[i-1], poly[i], poly[i+1]) per cell, with the
-// same device arithmetic as the in-kernel computation (bit-identical).
+// Each cell's polygon in the evaluation's rotated slot order (dev::Cell: slot j holds
+// poly[j-1], slot 0 poly[nv-1]) packed with its Wachspress numerator B_j = area(poly[j-1],
+// poly[j], poly[j+1]) -- the same device arithmetic as the in-kernel computation, so
+// bit-identical -- as one 32-B {x, y, z, B_j} per slot: the modes that re-read the polygon per
+// evaluation (pathline) load a slot with 2 VMEM instructions instead of a vertex double4 + B_j.
 template <int MAXV>
-__global__ void cell_b_kernel(int64_t C, const int* cellrec, const double4* vxyz, double* cellB) {
+__global__ void cell_poly_kernel(int64_t C, const int* cellrec, const double4* vxyz, double4* cpoly) {
     const int64_t c = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (c >= C) return;
     constexpr int REC = ((1 + 2 * MAXV) + 3) / 4 * 4;
@@ -2307,7 +2323,7 @@ __global__ void cell_b_kernel(int64_t C, const int* cellrec, const double4* vxyz
         if (k == nv - 1) { lx = x[k]; ly = y[k]; lz = z[k]; }
 #pragma unroll
     for (int i = 0; i < MAXV; ++i) {
-        double b = 0.0;
+        double4 o = make_double4(0.0, 0.0, 0.0, 0.0);
         if (i < nv) {
             const double qx = (i == 0) ? lx : x[(i + MAXV - 1) % MAXV];
             const double qy = (i == 0) ? ly : y[(i + MAXV - 1) % MAXV];
@@ -2316,9 +2332,9 @@ __global__ void cell_b_kernel(int64_t C, const int* cellrec, const double4* vxyz
             const double nx = wrap ? x[0] : x[(i + 1) % MAXV];
             const double ny = wrap ? y[0] : y[(i + 1) % MAXV];
             const double nz = wrap ? z[0] : z[(i + 1) % MAXV];
-            b = dev::tri_area(qx, qy, qz, x[i], y[i], z[i], nx, ny, nz);
+            o = make_double4(qx, qy, qz, dev::tri_area(qx, qy, qz, x[i], y[i], z[i], nx, ny, nz));
         }
-        cellB[c * MAXV + i] = b;
+        cpoly[c * MAXV + i] = o;
     }
 }
 
@@ -2544,7 +2560,7 @@ void free_mesh(mops_mesh* m) {
     if (!m) return;
     (void)hipFree(m->d_cellrec); (void)hipFree(m->d_cxyz); (void)hipFree(m->d_vxyz); (void)hipFree(m->d_cov);
     (void)hipFree(m->d_bary);
-    (void)hipFree(m->d_bkeys); (void)hipFree(m->d_bcells); (void)hipFree(m->d_hkeys); (void)hipFree(m->d_hval); (void)hipFree(m->d_cell_rank); (void)hipFree(m->d_cellB); (void)hipFree(m->d_rloc2); (void)hipFree(m->d_ring);
+    (void)hipFree(m->d_bkeys); (void)hipFree(m->d_bcells); (void)hipFree(m->d_hkeys); (void)hipFree(m->d_hval); (void)hipFree(m->d_cell_rank); (void)hipFree(m->d_cpoly); (void)hipFree(m->d_rloc2); (void)hipFree(m->d_ring);
     (void)hipFree(m->d_scratch);
     (void)hipFree(m->d_eoc); (void)hipFree(m->d_coe); (void)hipFree(m->d_exyz); (void)hipFree(m->d_rbf_coef);
     (void)hipFree(m->d_rbf_slot);
@@ -2836,11 +2852,11 @@ mops_status mops_mesh_create(const mops_mesh_desc* desc, void* stream, mops_mesh
     locate_radius_kernel<<<grid_for(C), kBlock, 0, s>>>(C, m->d_cxyz, bucket_dir(m), m->bucket_origin,
                                                         m->bucket_h, m->d_cellrec, m->rec_ints, m->maxv,
                                                         m->d_rloc2, m->d_ring);
-    if ((st = dmalloc(&m->d_cellB, (size_t)(C * m->maxv), &acc)) != MOPS_OK) { free_mesh(m); return st; }
+    if ((st = dmalloc(&m->d_cpoly, (size_t)(C * m->maxv), &acc)) != MOPS_OK) { free_mesh(m); return st; }
     switch (m->maxv) {
-        case 7: cell_b_kernel<7><<<grid_for(C), kBlock, 0, s>>>(C, m->d_cellrec, m->d_vxyz, m->d_cellB); break;
-        case 12: cell_b_kernel<12><<<grid_for(C), kBlock, 0, s>>>(C, m->d_cellrec, m->d_vxyz, m->d_cellB); break;
-        default: cell_b_kernel<20><<<grid_for(C), kBlock, 0, s>>>(C, m->d_cellrec, m->d_vxyz, m->d_cellB); break;
+        case 7: cell_poly_kernel<7><<<grid_for(C), kBlock, 0, s>>>(C, m->d_cellrec, m->d_vxyz, m->d_cpoly); break;
+        case 12: cell_poly_kernel<12><<<grid_for(C), kBlock, 0, s>>>(C, m->d_cellrec, m->d_vxyz, m->d_cpoly); break;
+        default: cell_poly_kernel<20><<<grid_for(C), kBlock, 0, s>>>(C, m->d_cellrec, m->d_vxyz, m->d_cpoly); break;
     }
     e = hipGetLastError();
     if (e == hipSuccess) e = hipStreamSynchronize(s);
@@ -3320,7 +3336,7 @@ mops_status mops_traj_advance(const mops_mesh* mesh, const mops_field* front, co
     a.mono1 = back ? back->d_mono : front->d_mono;
     a.order = p->d_order;
     a.n_live = p->d_n_live;
-    a.cellB = mesh->d_cellB;
+    a.cpoly = mesh->d_cpoly;
     a.px = p->d_x; a.py = p->d_y; a.pz = p->d_z; a.depth = p->d_depth; a.cell = p->d_cell; a.death = p->d_death_step;
     a.n = p->n;
     a.step_begin = step_begin; a.step_end = step_end; a.n_steps = n_steps;
