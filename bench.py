@@ -514,12 +514,7 @@ def main():
                      if pathline else None)
         cpu = cpu_baseline(mesh, snap, back_snap, seeds, seed_cells, args, n_steps)
 
-    if os.environ.get("MOPS_PROF_SECTIONS") == "1":  # experiment builds (-DMOPS_PROF) only
-        import ctypes
-        from mops_amd import _lib
-        buf = (ctypes.c_uint64 * 8)()
-        _lib.load().mops_debug_prof(buf)
-        print("prof counters lane-steps, lane walks, lane loads, wave-steps, wave-steps walking, wave-steps loading:", list(buf), file=sys.stderr)
+    print_prof_counters()
     if rank == 0:
         line = {
             "metric": "particle-steps/sec",
@@ -565,6 +560,17 @@ def main():
         print(json.dumps(line))
     if world > 1:
         dist.destroy_process_group()
+
+
+def print_prof_counters():
+    """Event counters of an experiment build (-DMOPS_PROF, MOPS_PROF_SECTIONS=1) to stderr."""
+    if os.environ.get("MOPS_PROF_SECTIONS") == "1":
+        import ctypes
+        from mops_amd import _lib
+        buf = (ctypes.c_uint64 * 8)()
+        _lib.load().mops_debug_prof(buf)
+        print("prof counters lane-steps, lane walks, lane loads, wave-steps, wave-steps walking, wave-steps loading:",
+              list(buf), file=sys.stderr)
 
 
 def main_chain(args, mesh, dev, world, rank):
@@ -667,6 +673,7 @@ def main_chain(args, mesh, dev, world, rank):
     if world > 1:
         dist.barrier()
     elapsed = time.perf_counter() - t0
+    print_prof_counters()
     kms = [a.elapsed_time(b) for (a, b) in timing]
     avg_kernel_s = (sum(kms) / len(kms)) / 1e3
     stats = torch.tensor([elapsed, float(attempted), float(n)], dtype=torch.float64,

@@ -70,6 +70,18 @@ constexpr int kPairRec = 10;  // doubles per level-pair record (see mops_field::
 #ifndef MOPS_PAIR_TEST
 #define MOPS_PAIR_TEST 1  // the walk's pair test (dev::walk)
 #endif
+#ifndef MOPS_PAIR_TEST_P
+#define MOPS_PAIR_TEST_P 1  // ... in the pathline kernels
+#endif
+// Compact per-lane LDS (traj_kernel): edge normals for polygon slots 0-5 only (slot 6, used by
+// heptagons alone, is computed in the evaluation: same operands, same bits) and the pair-test
+// radius as a float rounded toward zero (a smaller ball: the test stays conservative) --
+// 11.5 KB per 64-lane block instead of 13 KB.  Fuller LDS measured slower even at the same
+// 12 blocks per CU.
+#ifndef MOPS_LDS_COMPACT
+#define MOPS_LDS_COMPACT 1
+#endif
+constexpr int kNrmSlots(int maxv) { return (MOPS_LDS_COMPACT && maxv > 6) ? 6 : maxv; }
 #ifndef MOPS_PR_LEVEL_MAJOR
 #define MOPS_PR_LEVEL_MAJOR 1  // record (v, k) at index (k-1)*V + v (level-major; 0: v*(L-1) + k-1, vertex-major)
 #endif
@@ -478,11 +490,12 @@ struct Cell {
     // in a second, larger ball around it -- {n.x, n.y, n.z, k, rb2} at pr2[j * kTrajBlock] (LDS);
     // rb2 < 0 = none (load_cell)
     double* pr2;
+    float* rb2;      // MOPS_LDS_COMPACT: the pair test's rb2 (else pr2[4 * kTrajBlock])
     const double4* __restrict__ vxyz;   // rc == false: polygon re-read per evaluation (L1-resident)
     const double4* __restrict__ cpoly;  // rc == false: per-cell rotated polygon + B_i [C][MAXV] (cell_poly_kernel)
 };
 
-template <int MAXV, bool RC, bool NRM>
+template <int MAXV, bool RC, bool NRM, bool PT>
 __device__ __forceinline__ void load_cell(Cell<MAXV>& c, int cell, const int* __restrict__ cellrec,
                                           const double4* __restrict__ vxyz, const uint32_t* __restrict__ mono0,
                                           const uint32_t* __restrict__ mono1, const double4* __restrict__ cxyz,
@@ -493,7 +506,10 @@ __device__ __forceinline__ void load_cell(Cell<MAXV>& c, int cell, const int* __
         const double4 q = cxyz[cell];
         c.cx = q.x; c.cy = q.y; c.cz = q.z; c.rs2 = q.w;
     }
-    if constexpr (NRM && MOPS_PAIR_TEST) c.pr2[4 * kTrajBlock] = -1.0;  // no pair test before a walk in c
+    if constexpr (PT) {  // no pair test before a walk in c
+        if (MOPS_LDS_COMPACT) *c.rb2 = -1.0f;
+        else c.pr2[4 * kTrajBlock] = -1.0;
+    }
     constexpr int REC = ((1 + 2 * MAXV) + 3) / 4 * 4;
     const int* r = cellrec + (int64_t)cell * REC;
     int buf[REC];
@@ -535,7 +551,7 @@ __device__ __forceinline__ void load_cell(Cell<MAXV>& c, int cell, const int* __
         // edge normals: rotated slot pair i (see Cell) is (poly[i-1], poly[i]), poly[-1] = poly[nv-1]
 #pragma unroll
         for (int i = 0; i < MAXV; ++i) {
-            if (NRM && i < nv) {
+            if (NRM && i < nv && i < kNrmSlots(MAXV)) {
                 const double qx = (i == 0) ? lx : px[(i + MAXV - 1) % MAXV];
                 const double qy = (i == 0) ? ly : py[(i + MAXV - 1) % MAXV];
                 const double qz = (i == 0) ? lz : pz[(i + MAXV - 1) % MAXV];
@@ -631,7 +647,7 @@ __device__ __forceinline__ bool weights(const Cell<MAXV>& c, int L, int V, doubl
             const double by = wrap ? Y[0] : Y[(i + 1) % MAXV];
             const double bz = wrap ? Z[0] : Z[(i + 1) % MAXV];
             double nx, ny, nz;  // the edge normal X_i x X_{i+1}: cached per cell (load_cell) or computed
-            if (c.lds_n) {
+            if (c.lds_n && i < kNrmSlots(MAXV)) {
                 nx = c.nrm[(3 * i + 0) * kTrajBlock]; ny = c.nrm[(3 * i + 1) * kTrajBlock]; nz = c.nrm[(3 * i + 2) * kTrajBlock];
             } else {
                 nx = Y[i] * bz - Z[i] * by;
@@ -993,7 +1009,10 @@ __device__ __forceinline__ int walk(Cell<MAXV>& c, int cell, double x, double y,
             }
         }
     }
-    if constexpr (PAIR) c.pr2[4 * kTrajBlock] = rb2;
+    if constexpr (PAIR) {
+        if (MOPS_LDS_COMPACT) *c.rb2 = __double2float_rz(rb2);  // <= rb2: a conservative ball
+        else c.pr2[4 * kTrajBlock] = rb2;
+    }
     c.cx = x; c.cy = y; c.cz = z;
     return cell;
 }
@@ -1389,11 +1408,13 @@ __global__ void __launch_bounds__(kTrajBlock, (TrajWaves<MAXV, PATH, EULER>::val
     c.nv = 0;
     c.V = a.V;
     constexpr bool kRC = RCache<MAXV, PATH, EULER>::value, kNrm = LdsNormals<MAXV, PATH, EULER>::value;
-    __shared__ double s_nrm[kNrm ? 3 * MAXV * kTrajBlock : 1];  // per-lane edge normals (Cell::nrm)
+    __shared__ double s_nrm[kNrm ? 3 * kNrmSlots(MAXV) * kTrajBlock : 1];  // per-lane edge normals (Cell::nrm)
     c.nrm = s_nrm + threadIdx.x;
-    constexpr bool kPairT = kNrm && MOPS_PAIR_TEST;  // (load_cell resets it with the normals)
-    __shared__ double s_pr2[kPairT ? 5 * kTrajBlock : 1];  // per-lane pair test (Cell::pr2, dev::walk)
+    constexpr bool kPairT = kNrm && (PATH ? MOPS_PAIR_TEST_P : MOPS_PAIR_TEST);  // (load_cell resets it with the normals)
+    __shared__ double s_pr2[kPairT ? (MOPS_LDS_COMPACT ? 4 : 5) * kTrajBlock : 1];  // per-lane pair test (Cell::pr2, dev::walk)
+    __shared__ float s_rb2[kPairT && MOPS_LDS_COMPACT ? kTrajBlock : 1];
     c.pr2 = s_pr2 + threadIdx.x;
+    c.rb2 = s_rb2 + (kPairT && MOPS_LDS_COMPACT ? threadIdx.x : 0);
     const int C = a.C;
     // next recording step (the smallest j >= step_begin with (j+1) % rec_period == 0) and its
     // record index, advanced by counting instead of a 64-bit modulo per step
@@ -1407,7 +1428,7 @@ __global__ void __launch_bounds__(kTrajBlock, (TrajWaves<MAXV, PATH, EULER>::val
         MOPS_MARK(100);
         if (step == 0) {  // first_loop (:892-901)
             if (cell < 0 || cell >= C) { died = 0; break; }
-            dev::load_cell<MAXV, kRC, kNrm>(c, cell, a.cellrec, a.vxyz, a.mono0, a.mono1, a.cxyz, a.cpoly);
+            dev::load_cell<MAXV, kRC, kNrm, kPairT>(c, cell, a.cellrec, a.vxyz, a.mono0, a.mono1, a.cxyz, a.cpoly);
             double* r0 = a.rec;
             r0[0 * a.rec_stride + pid] = x;
             r0[1 * a.rec_stride + pid] = y;
@@ -1418,7 +1439,7 @@ __global__ void __launch_bounds__(kTrajBlock, (TrajWaves<MAXV, PATH, EULER>::val
             rec0 = true;
         } else {  // one-hop nearest-centre walk (:902-922)
             if (cell < 0 || cell >= C) { died = (int)step; break; }
-            if (c.id != cell) dev::load_cell<MAXV, kRC, kNrm>(c, cell, a.cellrec, a.vxyz, a.mono0, a.mono1, a.cxyz, a.cpoly);
+            if (c.id != cell) dev::load_cell<MAXV, kRC, kNrm, kPairT>(c, cell, a.cellrec, a.vxyz, a.mono0, a.mono1, a.cxyz, a.cpoly);
             // Exact shortcut: inside the stay ball around the anchor every
             // neighbour is strictly farther than c by more than rounding, so
             // the reference's argmin (c listed last, strict <) keeps c (dev::walk).
@@ -1427,7 +1448,7 @@ __global__ void __launch_bounds__(kTrajBlock, (TrajWaves<MAXV, PATH, EULER>::val
             const double e2p = ex * ex + ey * ey + ez * ez;
             bool stay_p = e2p < c.rs2;
             if constexpr (kPairT) {
-                if (!stay_p && e2p < c.pr2[4 * kTrajBlock])
+                if (!stay_p && e2p < (MOPS_LDS_COMPACT ? (double)*c.rb2 : c.pr2[4 * kTrajBlock]))
                     stay_p = c.pr2[0] * x + c.pr2[kTrajBlock] * y + c.pr2[2 * kTrajBlock] * z +
                              c.pr2[3 * kTrajBlock] > 0.0;
             }
@@ -1436,7 +1457,7 @@ __global__ void __launch_bounds__(kTrajBlock, (TrajWaves<MAXV, PATH, EULER>::val
             if (walking) {
                 cell = dev::walk<MAXV, kPairT>(c, cell, x, y, z, a.cellrec, a.cxyz, C);
                 loading = c.id != cell;
-                if (c.id != cell) dev::load_cell<MAXV, kRC, kNrm>(c, cell, a.cellrec, a.vxyz, a.mono0, a.mono1, a.cxyz, a.cpoly);
+                if (c.id != cell) dev::load_cell<MAXV, kRC, kNrm, kPairT>(c, cell, a.cellrec, a.vxyz, a.mono0, a.mono1, a.cxyz, a.cpoly);
             }
             {
                 const unsigned long long bw = __ballot(walking), bl = __ballot(loading), ba = __ballot(1);
@@ -1453,7 +1474,7 @@ __global__ void __launch_bounds__(kTrajBlock, (TrajWaves<MAXV, PATH, EULER>::val
             const double e2 = ex * ex + ey * ey + ez * ez;
             bool stay = e2 < c.rs2;
             if constexpr (kPairT) {
-                if (!stay && e2 < c.pr2[4 * kTrajBlock])  // second ball: only nb1 competes (dev::walk)
+                if (!stay && e2 < (MOPS_LDS_COMPACT ? (double)*c.rb2 : c.pr2[4 * kTrajBlock]))  // second ball: only nb1 competes (dev::walk)
                     stay = c.pr2[0] * x + c.pr2[kTrajBlock] * y + c.pr2[2 * kTrajBlock] * z +
                            c.pr2[3 * kTrajBlock] > 0.0;
             }
@@ -1471,7 +1492,7 @@ __global__ void __launch_bounds__(kTrajBlock, (TrajWaves<MAXV, PATH, EULER>::val
 #endif
                 cell = dev::walk<MAXV, kPairT>(c, cell, x, y, z, a.cellrec, a.cxyz, C);
                 if (c.id != cell) MOPS_CNT(5, 1);
-                if (c.id != cell) dev::load_cell<MAXV, kRC, kNrm>(c, cell, a.cellrec, a.vxyz, a.mono0, a.mono1, a.cxyz, a.cpoly);
+                if (c.id != cell) dev::load_cell<MAXV, kRC, kNrm, kPairT>(c, cell, a.cellrec, a.vxyz, a.mono0, a.mono1, a.cxyz, a.cpoly);
             }
 #endif
         }

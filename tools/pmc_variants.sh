@@ -1,5 +1,5 @@
 #!/bin/bash
-# One SQ counter pass per engine variant ("base" = the product library), bench.py config 2:
+# One SQ counter pass per engine variant ("base" = the product library), bench.py ${BENCH_ARGS} (default config 2):
 #   OUT=gpurun_out/x bash tools/pmc_variants.sh base nopair ...
 set -u
 out=${OUT:-gpurun_out/pmcv}
@@ -9,7 +9,7 @@ for v in "$@"; do
   if [ "$v" = base ]; then L=""; else L=$PWD/build/variants/libmops_$v.so; fi
   MOPS_TRAJ_LIB=$L timeout -s KILL 120 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS \
       SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_WAIT_INST_ANY SQ_BUSY_CYCLES --kernel-include-regex traj_kernel \
-      --output-format csv -d $out/$v -o p -- python3 bench.py --steps 1 --warmup 0 --no-cpu-baseline \
+      --output-format csv -d $out/$v -o p -- python3 bench.py --steps 1 --warmup 0 --no-cpu-baseline ${BENCH_ARGS:-} \
       > $out/$v.log 2>&1 || { echo "$v failed"; tail -5 $out/$v.log; exit 1; }
   python3 - $out/$v <<'PY'
 import csv, glob, sys, collections
