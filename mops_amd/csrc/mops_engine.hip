@@ -81,7 +81,10 @@ constexpr int kPairRec = 10;  // doubles per level-pair record (see mops_field::
 #ifndef MOPS_LDS_COMPACT
 #define MOPS_LDS_COMPACT 1
 #endif
-constexpr int kNrmSlots(int maxv) { return (MOPS_LDS_COMPACT && maxv > 6) ? 6 : maxv; }
+#ifndef MOPS_NRM_SLOTS
+#define MOPS_NRM_SLOTS 5  // polygon slots whose normals live in LDS (MOPS_LDS_COMPACT; slots 5-6 computed per evaluation)
+#endif
+constexpr int kNrmSlots(int maxv) { return (MOPS_LDS_COMPACT && maxv > MOPS_NRM_SLOTS) ? MOPS_NRM_SLOTS : maxv; }
 #ifndef MOPS_PR_LEVEL_MAJOR
 #define MOPS_PR_LEVEL_MAJOR 1  // record (v, k) at index (k-1)*V + v (level-major; 0: v*(L-1) + k-1, vertex-major)
 #endif
