@@ -607,3 +607,35 @@ def test_zlevel_topography_partial_bottom(gpu, engine_lib, oracle_lib, method):
         ref = oracle_lib.run(mesh, r0, rb, seeds, depths=depths, delta_t=120, duration=21600, record_t=1800,
                              euler=(method == "euler"), cells=got["cells"])
         assert_lines_match(got, ref, f"zlevel {method} path={back is not None}")
+
+
+def test_heptagon_cells_all_modes(gpu, engine_lib, oracle_lib):
+    """maxEdges 7 with heptagons (diagonal flips): the MAXV 7 kernels keep the IsInMesh
+    normals of polygon slots 0-4 in LDS and compute slots 5-6 per evaluation
+    (MOPS_LDS_COMPACT / MOPS_NRM_SLOTS), so seeds are placed in and around the
+    heptagon (and pentagon) cells; every mode bit-exact against the oracle."""
+    from mops_amd import synth
+    from mops_amd.engine import DeviceField, DeviceMesh, TrajectoryConfig, run_trajectories
+    mesh = synth.make_mesh(16, n_levels=10, flips=40)
+    nv = mesh.nEdgesOnCell.astype(np.int64)
+    odd = np.flatnonzero(nv != 6)
+    assert (nv == 7).sum() >= 10, "the test mesh must have heptagons"
+    rng = np.random.default_rng(5)
+    c = mesh.cellCoord[np.repeat(odd, 4)]
+    c = c + rng.normal(scale=2.0e4, size=c.shape)  # ~20 km around the odd cells' centres
+    c *= (synth.SEED_RADIUS / np.linalg.norm(c, axis=1))[:, None]
+    seeds = np.concatenate([c, synth.uniform_band_seeds(200, seed=43)])
+    s0 = synth.make_snapshot(mesh, timestep=0)
+    s1 = synth.make_snapshot(mesh, timestep=1, phase=0.35)
+    dm = DeviceMesh.from_mesh(mesh)
+    f0, f1 = DeviceField.from_snapshot(dm, s0), DeviceField.from_snapshot(dm, s1)
+    r0, r1 = oracle_lib.preprocess(mesh, s0), oracle_lib.preprocess(mesh, s1)
+    for back, rb in ((None, None), (f1, r1)):
+        for method in (1, 0):
+            cfg = TrajectoryConfig(deltaT=300, simulationDuration=43200, recordT=3600, depth=250.0, method=method)
+            got = run_trajectories(dm, f0, back, cfg, seeds)
+            ref = oracle_lib.run(mesh, r0, rb, seeds, depth=250.0, delta_t=300, duration=43200, record_t=3600,
+                                 euler=(method == 1), cells=got["cells"])
+            assert_lines_match(got, ref, f"heptagons path={back is not None} method={method}")
+            in_hept = np.isin(got["cells"], np.flatnonzero(nv == 7))
+            assert in_hept.sum() >= 20
