@@ -1,29 +1,27 @@
 #!/usr/bin/env python3
-"""Benchmark: particle-steps/sec of the MI355X StreamLine hot path.
+"""Benchmark: particle-steps/sec of the MI355X trajectory hot path.
 
-Workload (BASELINE.json configs[1]): EC30to60-class mesh (synthetic, ~236k
-ocean cells, 60 levels), 1e6 particles per GPU, fixed depth 800 m,
-dt = 120 s, 1-day streamline (720 steps, Euler = the reference default),
-records every 3600 s.  One bench "step" = one complete StreamLine call on
-the rank's particle shard: seed location, locality order, the 720 integration
-steps (2 particle parts x 6 step chunks on two streams), the line assembly +
-NaN cleanup (the reference's FinalizeTrajectoryLines) and -- for N > 1 -- an
-RCCL all-gather of the final-state checkpoint over xGMI on a side stream.
-``--gpus N`` without a launcher starts the N ranks itself (torch.distributed.run).
+Default workload (BASELINE.json configs[2], the largest config that fits one GPU): EC30to60-class
+mesh (synthetic, ~236k ocean cells, 60 levels), 1e7 particles per GPU, "layer 10" (mid-depth of
+0-based layer 10), dt = 60 s, 7-day pathline as 7 chained daily snapshot pairs (the reference's
+MOPSPathline.run, tutorial/pyMOPSAPI.py:1396-1531; mops_amd/chain.py), each pair's duration from the
+snapshots' timestamps.  One bench "step" = the whole 7-day chain: per pair the seed location
+(hinted by each particle's cell after pair 0), locality order, 1440 integration steps, the line
+assembly + NaN cleanup, and -- for N > 1 -- an RCCL all-gather of the pair's record slab (every
+particle's trajectory records, with seeds and slot ids) over xGMI on a side stream, overlapped
+with the next pair.  ``--gpus N`` without a launcher starts the N ranks itself.
 
-``--config 3``: BASELINE configs[2] -- 1e7 particles/GPU, layer 10, dt 60 s,
-7-day pathline as 7 chained daily snapshot pairs (mops_amd/chain.py).
+``--config 2``: BASELINE configs[1] -- 1e6 particles/GPU, depth 800 m, dt 120 s, 1-day streamline
+(720 Euler steps), records all-gathered after every call for N > 1.
 
-``--config 4``: BASELINE configs[3] -- oRRS18to6-class mesh (3.5M ocean cells,
-80 levels), 1e7 particles in total sharded over the ranks (strong scaling),
-depth 20 m, dt 120 s, 30-day pathline over 31 daily snapshots that are
-generated and derived in HBM inside the timed region (2 fields resident,
-~75 GB each), RCCL all-gather of the continuation points per pair.
+``--config 4``: BASELINE configs[3] -- oRRS18to6-class mesh (3.5M ocean cells, 80 levels), 1e7
+particles in total sharded over the ranks (strong scaling), depth 20 m, dt 120 s, 30-day pathline
+over 31 daily snapshots generated and derived in HBM inside the timed region (2 fields resident,
+~75 GB each).
 
-``--config 5``: BASELINE configs[4] -- same mesh, 1.25e7 Gaussian-seeded
-(Gulf-of-Mexico box) particles per GPU (weak scaling, 1e8 on 8 GPUs), dt 60 s,
-monthly snapshots; ``--pairs`` monthly pairs of the 365-day run (default 1 =
-a 30-day sample of the 12, stated in the JSON).
+``--config 5``: BASELINE configs[4] -- same mesh, 1.25e7 Gaussian-seeded (Gulf-of-Mexico box)
+particles per GPU (weak scaling, 1e8 on 8 GPUs), dt 60 s, 12 calendar-month pairs (Jan..Dec =
+365 days = 525 600 steps, daily records; ``--pairs k`` runs the first k months).
 
 Inputs (mesh, fields, seeds) are resident in HBM before the timed region.
 Rank 0 prints one JSON line (driver contract).
@@ -45,11 +43,11 @@ sys.path.insert(0, ROOT)
 PEAK_HBM_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md)
 
 
-def parse():
+def parse(argv=None):
     p = argparse.ArgumentParser()
     p.add_argument("--gpus", type=int, default=1)
-    p.add_argument("--steps", type=int, default=3)
-    p.add_argument("--warmup", type=int, default=1)
+    p.add_argument("--steps", type=int, default=None, help="timed steps (default per config: 3; config 5: 1)")
+    p.add_argument("--warmup", type=int, default=None, help="untimed steps (default per config: 1; config 5: 0)")
     p.add_argument("--particles", type=int, default=1_000_000, help="particles per GPU")
     p.add_argument("--freq", type=int, default=158, help="icosahedral frequency (158 -> ~236k ocean cells)")
     p.add_argument("--levels", type=int, default=60)
@@ -59,30 +57,30 @@ def parse():
     p.add_argument("--record", type=int, default=3600)
     p.add_argument("--method", choices=["euler", "rk4"], default="euler")
     p.add_argument("--mode", choices=["streamline", "pathline"], default="streamline",
-                   help="pathline: two snapshots (front/back), BASELINE config 3 shape")
-    p.add_argument("--config", type=int, choices=[2, 3, 4, 5], default=2,
-                   help="BASELINE.json config: 2 = 1e6-particle 1-day streamline (default); 3 = 1e7-particle "
-                        "7-day chained pathline at layer 10, dt 60 s; 4 = oRRS18to6-class 1e7-particle 30-day "
-                        "pathline (strong scaling); 5 = oRRS18to6-class 1.25e7 Gaussian particles/GPU, monthly "
-                        "pairs (weak scaling)")
+                   help="config 2 only: pathline = two snapshots (front/back) on the config-2 mesh")
+    p.add_argument("--config", type=int, choices=[2, 3, 4, 5], default=3,
+                   help="BASELINE.json config: 3 = 1e7-particle 7-day chained pathline at layer 10, dt 60 s (default: "
+                        "the largest single-GPU config); 2 = 1e6-particle 1-day streamline; 4 = oRRS18to6-class "
+                        "1e7-particle 30-day pathline (strong scaling); 5 = oRRS18to6-class 1.25e7 Gaussian "
+                        "particles/GPU, 12 calendar-month pairs (weak scaling)")
     p.add_argument("--pairs", type=int, default=None,
-                   help="configs 3/4/5: snapshot pairs (defaults 7 daily / 30 daily / 1 monthly of 12)")
+                   help="configs 3/4/5: snapshot pairs (defaults 7 daily / 30 daily / 12 monthly)")
     p.add_argument("--backend", choices=["nccl", "gloo"], default="nccl",
                    help="collective backend for N > 1 (nccl = RCCL over xGMI; gloo only to rehearse the multi-rank "
                         "path on one GPU with MOPS_BENCH_ONE_DEVICE=1)")
     p.add_argument("--segment", type=int, default=0,
-                   help="integration steps per kernel launch (config 2: whole record periods; 0 = the whole "
-                        "run at N=1, a quarter of it at N>1 so record all-gathers overlap the next launch; "
-                        "chains: 0 = launches of 3 simulated days with a locality re-sort between them)")
+                   help="integration steps per kernel launch (config 2: whole record periods, 0 = the whole "
+                        "run; chains: 0 = launches of 3 simulated days with a locality re-sort between them)")
     p.add_argument("--parts", type=int, default=2,
                    help="config 2: particle parts on their own streams (ParticleSet.advance_pipelined)")
     p.add_argument("--chunks", type=int, default=6,
                    help="config 2: step chunks per part and segment (shorter launches whose tails overlap)")
-    p.add_argument("--gather", choices=["checkpoint", "records"], default="checkpoint",
-                   help="config 2, N > 1: 'checkpoint' = one all-gather per call of every particle's final state "
-                        "(position, depth, death) + slot ids -- particles are independent, so the path itself "
-                        "needs no exchange and each rank keeps its shard's records; 'records' = all-gather every "
-                        "record slab as well (1.15 GB per rank per call), overlapped with the next quarter run")
+    p.add_argument("--gather", choices=["records", "checkpoint"], default="records",
+                   help="N > 1: 'records' (default, the north star's trajectory collection) = at every checkpoint "
+                        "(the end of a config-2 call, the end of each chained pair) one all-gather of every rank's "
+                        "record slab + seeds + slot ids (distributed.RecordGather), overlapped with the next call / "
+                        "pair; 'checkpoint' = only every particle's final state (position, depth, death, id) / the "
+                        "pair's continuation points")
     p.add_argument("--topography", choices=["sigma", "zlevel"], default="sigma",
                    help="config 2: synthetic vertical grid (synth.make_snapshot): 'zlevel' = MPAS-O z-levels with "
                         "partial bottom cells and zero-thickness inactive levels")
@@ -100,17 +98,34 @@ def parse():
                    help="run the compaction re-sorts on high-priority streams (experiment)")
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--cpu-seconds", type=float, default=12.0, help="target CPU-baseline sample length")
-    return p.parse_args()
+    return p.parse_args(argv)
+
+
+STEPS_DEFAULT = {2: (3, 1), 3: (3, 1), 4: (2, 1), 5: (1, 0)}  # (steps, warmup)
+
+
+def apply_config_defaults(args):
+    """Fill the options left at their config-2 defaults with the chosen config's values (and the
+    per-config steps / warmup)."""
+    if args.config in (3, 4, 5):
+        d = vars(argparse.Namespace(mode="streamline", particles=1_000_000, dt=120, duration=86400, record=3600,
+                                    method="euler", depth=800.0, freq=158, levels=60))
+        for k, v in {3: CONFIG3, 4: CONFIG4, 5: CONFIG5}[args.config].items():
+            if getattr(args, k) == d[k]:
+                setattr(args, k, v)
+        if args.pairs is None:
+            args.pairs = PAIRS_DEFAULT[args.config]
+    st, wu = STEPS_DEFAULT[args.config]
+    if args.steps is None:
+        args.steps = st
+    if args.warmup is None:
+        args.warmup = wu
+    return args
 
 
 def all_gather_flat(dist, out, inp, backend):
-    """One all-gather of a rank's slab; gloo (rehearsal only) stages through host memory."""
-    if backend == "nccl":
-        dist.all_gather_into_tensor(out, inp)
-    else:
-        o = out.cpu()
-        dist.all_gather_into_tensor(o, inp.cpu())
-        out.copy_(o)
+    from mops_amd.distributed import all_gather_flat as agf
+    agf(dist, out, inp, backend)
 
 
 def make_seeds(n: int, rank: int) -> np.ndarray:
@@ -244,12 +259,30 @@ def algorithmic_bytes_per_pstep(nv: float, L: int, S: int = 1) -> float:
 
 
 CONFIG3 = dict(mode="pathline", particles=10_000_000, dt=60, duration=86400, record=3600, method="euler")
+# (configs 3-5: `duration` is the daily snapshot spacing; config 5's snapshots are monthly -- each pair's
+# duration comes from its calendar month, chain_timestamps)
 # oRRS18to6 class: frequency-608 icosahedral dual (3.7M cells, 3.5M after the land cull), 80 levels
 CONFIG4 = dict(mode="pathline", particles=10_000_000, dt=120, duration=86400, record=3600, method="euler",
                depth=20.0, freq=608, levels=80)
-CONFIG5 = dict(mode="pathline", particles=12_500_000, dt=60, duration=30 * 86400, record=30 * 86400,
+CONFIG5 = dict(mode="pathline", particles=12_500_000, dt=60, duration=30 * 86400, record=86400,
                method="euler", depth=20.0, freq=608, levels=80)
-PAIRS_DEFAULT = {3: 7, 4: 30, 5: 1}
+PAIRS_DEFAULT = {3: 7, 4: 30, 5: 12}
+
+
+def chain_timestamps(config: int, pairs: int, spacing: int = 86400) -> list:
+    """MPAS xtime of the chain's snapshots: daily from 0001-01-01 (configs 3/4), or the first day of
+    each month from January 0001 (config 5: calendar-month pairs, MOPSPathline._month_pairs_forward);
+    the chain derives each pair's simulationDuration from them (chain.pair_gaps)."""
+    from mops_amd import chain
+    if config == 5:
+        mp = chain.month_pairs_forward(1, 1, 1 + (pairs // 12) + 1, 12)[:pairs]
+        if len(mp) != pairs:
+            raise ValueError("month pairs")
+        return chain.month_timestamps(mp)
+    from datetime import datetime, timedelta
+    t0 = datetime(1, 1, 1)
+    return [(t0 + timedelta(seconds=spacing * i)).strftime("%Y-%m-%d_%H:%M:%S").rjust(19, "0")
+            for i in range(pairs + 1)]
 
 
 def layer_mid_depth(mesh, layer: int = 10) -> float:
@@ -286,14 +319,7 @@ def main():
         import subprocess
         sys.exit(subprocess.run(launcher_command(args.gpus, sys.argv[1:], free_port())).returncode)
     check_world(args.gpus, int(os.environ.get("WORLD_SIZE", "1")))
-    if args.config in (3, 4, 5):  # config values for every option left at its config-2 default
-        d = vars(argparse.Namespace(mode="streamline", particles=1_000_000, dt=120, duration=86400, record=3600,
-                                    method="euler", depth=800.0, freq=158, levels=60))
-        for k, v in {3: CONFIG3, 4: CONFIG4, 5: CONFIG5}[args.config].items():
-            if getattr(args, k) == d[k]:
-                setattr(args, k, v)
-        if args.pairs is None:
-            args.pairs = PAIRS_DEFAULT[args.config]
+    apply_config_defaults(args)
     import torch
     import torch.distributed as dist
 
@@ -311,6 +337,7 @@ def main():
             dist.init_process_group("gloo")
 
     from mops_amd import synth
+    from mops_amd.distributed import RecordGather
     from mops_amd.engine import DeviceField, DeviceMesh, ParticleSet, TrajectoryConfig
 
     mesh = synth.make_mesh(args.freq, n_levels=args.levels)
@@ -334,54 +361,38 @@ def main():
     period = ps.record_period(pathline=pathline)
     n_steps = cfg.n_steps
     # launches: the whole run as one segment (every launch re-reads the particle state and
-    # re-loads each particle's cell stencil: 30-step launches cost 6% at config 2); with
-    # --gather records at N>1, quarters of the run whose records are all-gathered while the next
-    # quarter computes, and a final one-record segment so that only one record's gather is exposed
-    gather_records = world > 1 and args.gather == "records"
-    seg = args.segment if args.segment > 0 else (period * max(1, ps.K // 4) if gather_records else n_steps)
+    # re-loads each particle's cell stencil: 30-step launches cost 6% at config 2)
+    seg = args.segment if args.segment > 0 else n_steps
     seg = max(period, (seg // period) * period)  # whole record periods per launch
     bounds = list(range(0, n_steps, seg)) + [n_steps]
-    if args.segment <= 0 and gather_records and bounds[-1] - bounds[-2] > period:
-        bounds.insert(-1, bounds[-1] - period)
     segments = [(bounds[i], bounds[i + 1]) for i in range(len(bounds) - 1)]
     compute = torch.cuda.Stream(dev)
     comm = torch.cuda.Stream(dev)
     part_streams = [torch.cuda.Stream(dev) for _ in range(max(1, args.parts))]
-    gathered = gathered_ids = ckpt = gathered_ckpt = None
-    if world > 1:
-        # everything is gathered in each rank's slot (locality) order, with the rank's slot ->
-        # particle ids once per call, so it maps back to particles (distributed.unshard_slots)
-        gathered_ids = torch.empty((world, n), dtype=torch.int32, device=dev)
-        ckpt = torch.empty((5, n), dtype=torch.float64, device=dev)  # x, y, z, depth, death step
-        gathered_ckpt = torch.empty((world, 5, n), dtype=torch.float64, device=dev)
-        if gather_records:
-            gathered = torch.empty((ps.K, world, 6, n), dtype=torch.float64, device=dev)
+    gather_records = world > 1 and args.gather == "records"
+    collector = ckpt = gathered_ckpt = None
+    if world > 1 and gather_records:
+        # every call's record slab + seeds + slot ids, all-gathered on `comm` while the next call computes
+        collector = RecordGather(dist, ps, world, backend=args.backend, comm_stream=comm)
+    elif world > 1:
+        ckpt = torch.empty((6, n), dtype=torch.float64, device=dev)  # x, y, z, depth, death step, slot id
+        gathered_ckpt = torch.empty((world, 6, n), dtype=torch.float64, device=dev)
 
     kernel_ms = []
     finalize_ms = []  # line assembly + NaN cleanup per call
     lines_out = [None]  # the last call's finalized lines (kept alive until the next call)
     compact = args.compact == "on" or (args.compact == "auto" and args.method == "rk4")
     dispatch_ms = []  # per traj_kernel launch (HIP events on its part stream): what rocprofv3 averages
-    ev_ids, ev_ckpt = [None], [None]  # comm-stream events of the last slot-id / checkpoint gathers
+    ev_ckpt = [None]  # comm-stream event of the last checkpoint gather
 
     def one_call(timed: bool, pset=None):
         """One StreamLine call on this rank's shard (device resident); ``pset``: another ParticleSet
         of the same seeds (the RK4 companion line)."""
         ps_ = pset if pset is not None else ps
         with torch.cuda.stream(compute):
-            if ev_ids[0] is not None:  # the previous call's slot-id gather has read ids (reorder rewrites them)
-                compute.wait_event(ev_ids[0])
             ps_.reset(depth=args.depth)
             dmesh.locate(ps_.seeds.data_ptr(), ps_.cell.data_ptr(), n, stream=compute)  # seeds in slot order
             ps_.reorder(stream=compute)
-            if world > 1:
-                sorted_ev = torch.cuda.Event()
-                sorted_ev.record(compute)
-                comm.wait_event(sorted_ev)
-                with torch.cuda.stream(comm):
-                    all_gather_flat(dist, gathered_ids.view(-1), ps_.ids, args.backend)
-                    ev_ids[0] = torch.cuda.Event()
-                    ev_ids[0].record(comm)
             for (s0, s1) in segments:
                 # the segment's trajectory launches: particle parts on their own streams, each in
                 # step chunks, so one part's final partial round of waves overlaps the others' work
@@ -389,8 +400,6 @@ def main():
                 e0.record(compute)
                 for st in part_streams:
                     st.wait_event(e0)
-                # step chunks in proportion to the segment's share of the run (N > 1 runs quarter
-                # segments whose record gathers overlap the next one: short launches cost ~6% each)
                 nch = max(1, round(args.chunks * (s1 - s0) / n_steps))
                 ps_.advance_pipelined(dfield, dback, s0, s1, part_streams, nch,
                                      timing=dispatch_ms if timed else None,
@@ -414,32 +423,27 @@ def main():
                         lines_out[0] = ps_.finalize(pathline, stream=compute, timing=fin)
                     if timed:
                         finalize_ms.append(fin)
-                if gather_records:  # the records this segment completed, gathered while the next one computes
-                    k0, k1 = s0 // period, min(s1 // period, ps_.K)
-                    if k1 > k0:
-                        done = torch.cuda.Event()
-                        done.record(compute)
-                        comm.wait_event(done)
-                        with torch.cuda.stream(comm):
-                            for k in range(k0, k1):
-                                all_gather_flat(dist, gathered[k].view(-1), ps_.records[k].view(-1), args.backend)
-            if world > 1:  # the checkpoint: every particle's final state on every rank
-                if ev_ckpt[0] is not None:  # the previous call's checkpoint gather has read ckpt
-                    compute.wait_event(ev_ckpt[0])
-                ckpt[0].copy_(ps_.x); ckpt[1].copy_(ps_.y); ckpt[2].copy_(ps_.z)
-                ckpt[3].copy_(ps_.depth); ckpt[4].copy_(ps_.death)
-                done = torch.cuda.Event()
-                done.record(compute)
-                comm.wait_event(done)
-                with torch.cuda.stream(comm):
-                    all_gather_flat(dist, gathered_ckpt.view(-1), ckpt.view(-1), args.backend)
-                    ev_ckpt[0] = torch.cuda.Event()
-                    ev_ckpt[0].record(comm)
+            # (every re-sort and compaction of the call is done: the slot ids, seeds and records below are
+            # in one consistent slot order -- ADVICE r3: ids gathered right after the first sort went stale
+            # once the compactions permuted the slots)
+            if world > 1 and pset is None:
+                if gather_records:
+                    collector.collect(ps_, compute)  # records + seeds + ids; ps_ moves to the spare slab
+                else:  # the checkpoint: every particle's final state (+ its slot id) on every rank
+                    if ev_ckpt[0] is not None:  # the previous call's checkpoint gather has read ckpt
+                        compute.wait_event(ev_ckpt[0])
+                    ckpt[0].copy_(ps_.x); ckpt[1].copy_(ps_.y); ckpt[2].copy_(ps_.z)
+                    ckpt[3].copy_(ps_.depth); ckpt[4].copy_(ps_.death); ckpt[5].copy_(ps_.ids)
+                    done = torch.cuda.Event()
+                    done.record(compute)
+                    comm.wait_event(done)
+                    with torch.cuda.stream(comm):
+                        all_gather_flat(dist, gathered_ckpt.view(-1), ckpt.view(-1), args.backend)
+                        ev_ckpt[0] = torch.cuda.Event()
+                        ev_ckpt[0].record(comm)
         compute.synchronize()
-        if gather_records:  # the next call's reset rewrites the records these gathers read
-            comm.synchronize()
-        # checkpoint mode: this call's checkpoint gather overlaps the next call's compute (the events
-        # above order the buffers); the timed region's closing device synchronize waits for the last one
+        # the gathers overlap the next call's compute (events order the buffers); the timed region's
+        # closing device synchronize waits for the last one
 
     for _ in range(args.warmup):
         one_call(False)
@@ -530,17 +534,13 @@ def main():
             "dtype": "f64",
             "data": "synthetic (icosahedral-dual Voronoi mesh, analytic flow; no MPAS files offline)",
             "config": {
-                "workload": (f"EC30to60-class {args.mode}, {n:.0e} particles/GPU, depth {args.depth:g} m, "
-                             f"dt {args.dt} s, {args.duration / 86400:g} day"),
+                "workload": (f"EC30to60-class {args.mode} (BASELINE config 2), {n:.0e} particles/GPU, depth "
+                             f"{args.depth:g} m, dt {args.dt} s, {args.duration / 86400:g} day"),
                 "cells": mesh.nCells, "vertices": mesh.nVertices, "levels": mesh.nVertLevels,
                 "particles_per_gpu": n, "particles_total": int(n_all), "integration_steps": n_steps,
                 "records": ps.K, "method": args.method, "parallelism": f"particle-shard x{world}",
                 "topography": args.topography,
-                "record_gather": ("none" if world == 1 else
-                                  f"{'rccl' if args.backend == 'nccl' else 'gloo'} all_gather of the final-state "
-                                  "checkpoint (+ slot ids) per call" + (
-                                      " and of every record slab, overlapped with the next quarter run"
-                                      if gather_records else "; records stay sharded on their rank")),
+                "record_gather": record_gather_text(world, args, per="call", K=ps.K, collector=collector),
             },
             "nominal_particle_steps_per_call": n_all * n_steps,
             "attempted_particle_steps_per_call": attempted_all,
@@ -562,6 +562,25 @@ def main():
         dist.destroy_process_group()
 
 
+def record_gather_text(world: int, args, per: str, K: int, collector=None) -> str:
+    """What the N > 1 line collects (the bench line states it)."""
+    if world == 1:
+        return "none (one rank: its lines are assembled on the device every " + per + ")"
+    be = "rccl" if args.backend == "nccl" else "gloo"
+    if args.gather == "records":
+        txt = (f"{be} all_gather at every {per} of each rank's record slab ({K} records x 48 B per particle, in slot "
+               "order) + seeds + slot ids (distributed.RecordGather): every rank holds every particle's trajectory "
+               "records, overlapped with the next " + per)
+        if collector is not None:
+            txt += f"; {collector.bytes_per_rank / max(1, collector.checkpoints) / 1e9:.3f} GB sent per rank per {per}"
+            if collector.chunk < collector.shape[0]:
+                txt += (f", in chunks of {collector.chunk} records through a {collector.gathered.numel() * 8 / 1e9:.1f} GB "
+                        "ring (the whole gathered slab does not fit beside the fields)")
+        return txt
+    return (f"{be} all_gather at every {per} of the final state / continuation points (+ slot ids); records stay "
+            "sharded on their rank")
+
+
 def print_prof_counters():
     """Event counters of an experiment build (-DMOPS_PROF, MOPS_PROF_SECTIONS=1) to stderr."""
     if os.environ.get("MOPS_PROF_SECTIONS") == "1":
@@ -574,26 +593,31 @@ def print_prof_counters():
 
 
 def main_chain(args, mesh, dev, world, rank):
-    """BASELINE configs 3-5: chained snapshot-pair pathlines (MOPSPathline.run semantics, mops_amd/chain.py).
+    """BASELINE configs 3-5: chained snapshot-pair pathlines (MOPSPathline.run semantics, mops_amd/chain.py),
+    each pair's simulationDuration from the snapshots' timestamps (daily for configs 3/4, calendar months
+    for config 5).
 
     config 3: 1e7 particles/GPU, "layer 10", dt 60 s, 7 daily pairs; all 8 derived snapshots are resident in
     HBM before the timed region.  configs 4/5: oRRS18to6-class mesh; each snapshot is generated and derived in
     HBM inside the timed region (mops_field_create_device), two fields resident.  One bench step = the whole
-    chain (seed locate per pair, every integration step, per-pair line assembly on device, an RCCL all-gather
-    of each pair's continuation points when N > 1)."""
+    chain (seed locate per pair, every integration step, per-pair line assembly on device, and for N > 1 an
+    RCCL all-gather of each pair's record slab + seeds + slot ids, overlapped with the next pair)."""
     import torch
     import torch.distributed as dist
     from mops_amd import synth
-    from mops_amd.chain import PathlineChain
+    from mops_amd.chain import PathlineChain, pair_gaps
+    from mops_amd.distributed import RecordGather, max_shard, shard_bounds
     from mops_amd.engine import DeviceField, DeviceMesh
 
     n_snap = args.pairs + 1
+    stamps = chain_timestamps(args.config, args.pairs, spacing=args.duration)
+    gaps = pair_gaps(stamps)
     dmesh = DeviceMesh.from_mesh(mesh)
     snaps = None
     if args.config == 3:
         snaps = [synth.make_snapshot(mesh, timestep=t, phase=0.35 * t) for t in range(n_snap)]
         fields = [DeviceField.from_snapshot(dmesh, s) for s in snaps]
-        chain = PathlineChain(dmesh, lambda i, stream: fields[i], n_snap, gap_seconds=args.duration, device=dev,
+        chain = PathlineChain(dmesh, lambda i, stream: fields[i], n_snap, timestamps=stamps, device=dev,
                               own_fields=False)
     else:
         from mops_amd.synth_device import DeviceFieldRecycler, DeviceSnapshotSource
@@ -613,39 +637,50 @@ def main_chain(args, mesh, dev, world, rank):
             recycler.release(b)
         del bufs
         torch.cuda.synchronize()
-        chain = PathlineChain(dmesh, recycler, n_snap, gap_seconds=args.duration,
+        chain = PathlineChain(dmesh, recycler, n_snap, timestamps=stamps,
                               device=dev, own_fields=True, prefetch=False, overlap_stream=overlap)
         chain.overlap_stream_cus = side_cus
     if args.config == 4:  # strong scaling: 1e7 particles in total, one contiguous shard per rank
         allseeds = make_seeds(args.particles, 0)
-        lo, hi = len(allseeds) * rank // world, len(allseeds) * (rank + 1) // world
+        lo, hi = shard_bounds(len(allseeds), rank, world)
         seeds = allseeds[lo:hi]
+        n_pad = max_shard(len(allseeds), world)
         del allseeds
-    elif args.config == 5:
-        seeds = make_gaussian_seeds(args.particles, rank)
     else:
-        seeds = make_seeds(args.particles, rank)
+        seeds = make_gaussian_seeds(args.particles, rank) if args.config == 5 else make_seeds(args.particles, rank)
+        n_pad = seeds.shape[0]
     n = seeds.shape[0]
     compute = torch.cuda.Stream(dev)
     if args.config in (4, 5) and chain.overlap_stream is not None:
         compute = compute_masked  # the trajectory launches leave the side stream's CUs free
     comm = torch.cuda.Stream(dev)
-    n_pad = n
-    if world > 1:  # equal-size all-gather buffers (config-4 shards may differ by one particle)
-        t = torch.tensor([n], dtype=torch.int64, device=dev if args.backend == "nccl" else "cpu")
+    if world > 1 and args.config != 4:  # weak scaling: every rank must hold the same particle count
+        t = torch.tensor([n, -n], dtype=torch.int64, device=dev if args.backend == "nccl" else "cpu")
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        n_pad = int(t.item())
+        if int(t[0].item()) != -int(t[1].item()):
+            raise SystemExit("bench.py: ranks drew different particle counts")
+    gather_records = world > 1 and args.gather == "records"
     gathered = torch.empty((world, n_pad, 3), dtype=torch.float64, device=dev) if world > 1 else None
     send = torch.zeros((n_pad, 3), dtype=torch.float64, device=dev) if world > 1 else None
+    collector = [None]
     timing = []
 
     t_start = [time.perf_counter()]
 
-    def on_pair(p, last):
+    def on_pair(p, last, ps):
         if rank == 0 and args.pairs > 7:  # progress for long chains (stderr)
             print(f"[bench] pair {p + 1}/{args.pairs} enqueued at {time.perf_counter() - t_start[0]:.1f} s",
                   file=sys.stderr, flush=True)
-        if world > 1:  # checkpoint: every rank gets the continuation points of all shards
+        if gather_records:  # the pair's trajectory records (+ seeds, slot ids) on every rank
+            if collector[0] is None:
+                # the ring of gathered records must fit beside the fields (config 5 at 8 ranks gathers 149 GB
+                # per pair: chunks of records through a bounded ring, RecordGather(max_bytes))
+                free, _ = torch.cuda.mem_get_info(dev)
+                budget = int(0.6 * (free - 2 * ps.records.numel() * 8))
+                collector[0] = RecordGather(dist, ps, world, backend=args.backend, comm_stream=comm,
+                                            max_bytes=max(budget, 1 << 30))
+            collector[0].collect(ps, compute)
+        elif world > 1:  # checkpoint: every rank gets the continuation points of all shards
             done = torch.cuda.Event(); done.record(compute)
             comm.wait_event(done)
             last.record_stream(comm)
@@ -656,7 +691,8 @@ def main_chain(args, mesh, dev, world, rank):
     def one_call(timed):
         res = chain.run(seeds, depth=args.depth, method=1 if args.method == "euler" else 0, delta_t=args.dt,
                         record_t=args.record, keep_lines=False, compute_stream=compute, on_pair=on_pair,
-                        timing=timing if timed else None, segment_steps=args.segment if args.segment else -1)
+                        timing=timing if timed else None, segment_steps=args.segment if args.segment else -1,
+                        record_stride=n_pad)
         compute.synchronize(); comm.synchronize()
         return res
 
@@ -684,7 +720,7 @@ def main_chain(args, mesh, dev, world, rank):
         elapsed, attempted_all, n_all = mx[0].item(), sm[1].item(), sm[2].item()
     else:
         attempted_all, n_all = float(attempted), float(n)
-    n_steps = args.pairs * (args.duration // args.dt)
+    n_steps = sum(g // args.dt for g in gaps)
     value = attempted_all / elapsed
     nv_mean = float(np.mean(mesh.nEdgesOnCell.astype(np.float64)))
     B = algorithmic_bytes_per_pstep(nv_mean, mesh.nVertLevels, 2)
@@ -692,7 +728,7 @@ def main_chain(args, mesh, dev, world, rank):
     psteps_per_launch = attempted / args.steps / launches_per_call
     mesh_class = "EC30to60" if args.config == 3 else "oRRS18to6"
     from mops_amd.chain import REORDER_SECONDS
-    seg_key = args.segment if args.segment > 0 else min(args.duration // args.dt, REORDER_SECONDS // args.dt)
+    seg_key = args.segment if args.segment > 0 else min(gaps[0] // args.dt, REORDER_SECONDS // args.dt)
     roof = roofline_block(f"traj_kernel<7,true,{str(args.method == 'euler').lower()}> (pathline {args.method})",
                           avg_kernel_s, psteps_per_launch, B,
                           f"{mesh_class.lower()}_chain{args.config}_{args.method}_{args.particles}_seg{seg_key}")
@@ -701,20 +737,22 @@ def main_chain(args, mesh, dev, world, rank):
         seed_cells = dmesh_locate_host(dmesh, seeds, dev)
         if snaps is None:  # configs 4/5: the first pair's snapshots, built on the host for the oracle
             snaps = [synth.make_snapshot(mesh, timestep=t, phase=0.35 * t) for t in range(2)]
-        cpu = cpu_baseline(mesh, snaps[0], snaps[1], seeds, seed_cells, args, args.duration // args.dt)
+        cpu = cpu_baseline(mesh, snaps[0], snaps[1], seeds, seed_cells, args, gaps[0] // args.dt,
+                           duration=gaps[0])
+    days = sum(gaps) / 86400
     if args.config == 3:
         workload = (f"EC30to60-class chained pathline (BASELINE config 3), {n:.0e} particles/GPU, layer 10 "
-                    f"({args.depth:.1f} m), dt {args.dt} s, {args.pairs} days = {args.pairs} daily pairs")
+                    f"({args.depth:.1f} m), dt {args.dt} s, {days:g} days = {args.pairs} daily pairs")
     elif args.config == 4:
         workload = (f"oRRS18to6-class chained pathline (BASELINE config 4), {int(n_all):.0e} particles in total "
-                    f"({n} on this rank), depth {args.depth:g} m, dt {args.dt} s, {args.pairs} days = {args.pairs} "
+                    f"({n} on this rank), depth {args.depth:g} m, dt {args.dt} s, {days:g} days = {args.pairs} "
                     "daily pairs, snapshots generated + derived in HBM inside the timed region")
     else:
         workload = (f"oRRS18to6-class chained pathline (BASELINE config 5), {n:.3g} Gaussian Gulf-of-Mexico particles"
                     f"/GPU, depth {args.depth:g} m, dt {args.dt} s, "
-                    + (f"all {args.pairs} monthly pairs of the year-long run" if args.pairs >= 12 else
-                       f"{args.pairs} monthly pair(s) of the 12 in the year-long run (a bounded sample; every pair "
-                       "is the same work shape)")
+                    + (f"all {args.pairs} calendar-month pairs of the year ({days:g} days)" if args.pairs >= 12 else
+                       f"the first {args.pairs} calendar-month pair(s) of the year ({days:g} days; a bounded "
+                       "sample of the 12)")
                     + ", snapshots generated + derived in HBM inside the timed region")
     if rank == 0:
         print(json.dumps({
@@ -727,12 +765,13 @@ def main_chain(args, mesh, dev, world, rank):
                 "workload": workload,
                 "cells": mesh.nCells, "vertices": mesh.nVertices, "levels": mesh.nVertLevels,
                 "particles_per_gpu": n, "particles_total": int(n_all), "integration_steps": n_steps,
-                "records_per_pair": args.duration // args.record, "method": args.method,
-                "parallelism": f"particle-shard x{world}",
+                "snapshot_times": [stamps[0], stamps[-1]], "pair_seconds": sorted(set(gaps)),
+                "records_per_pair": sorted({g // args.record for g in gaps}), "record_t": args.record,
+                "method": args.method, "parallelism": f"particle-shard x{world}",
                 "snapshot_overlap": (f"snapshot p+2 generated + derived on a {chain.overlap_stream_cus}-CU side stream "
                                      "during pair p (3 field buffers)") if chain.overlap_stream is not None else "none",
-                "record_gather": (f"{'rccl' if args.backend == 'nccl' else 'gloo'} all_gather of continuation points "
-                                  "per pair") if world > 1 else "none"},
+                "record_gather": record_gather_text(world, args, per="pair", K=max(g // args.record for g in gaps),
+                                                    collector=collector[0])},
             "nominal_particle_steps_per_call": n_all * n_steps,
             "attempted_particle_steps_per_call": attempted_all / args.steps,
             "roofline": roof,
@@ -751,33 +790,65 @@ def dmesh_locate_host(dmesh, seeds, dev):
     return c.cpu().numpy()
 
 
-def cpu_baseline(mesh, snap, back_snap, seeds, cells, args, n_steps):
-    """The CPU oracle (port of the TBB path) on this host's cores, bounded sample."""
+CPU_CALIBRATION = os.path.join(ROOT, "profiles", "r04", "cpu_calibration.json")
+
+
+def cpu_calibration(threads: int):
+    """The port's speed relative to the reference's own TBB path (tools/calibrate_cpu.py: the port timed on the
+    survey's probe shape in the build container, against the survey's timings of the reference built there),
+    for the thread count closest to ``threads``."""
+    try:
+        cal = json.load(open(CPU_CALIBRATION))
+    except (OSError, ValueError):
+        return None
+    runs = [r for r in cal.get("runs", []) if r.get("method") == "euler"]
+    if not runs:
+        return None
+    r = min(runs, key=lambda r: abs(r["threads"] - threads))
+    return {"port_over_reference": r["port_speed_over_reference"], "threads": r["threads"],
+            "source": f"profiles/r04/cpu_calibration.json (tools/calibrate_cpu.py): the port {r['port_us_per_nominal_pstep']:.3f} "
+                      f"vs the reference {r['reference_us_per_pstep_survey']:.3f} us per particle-step, Euler streamline, "
+                      f"{cal['mesh']['cells']} cells x {cal['mesh']['levels']} levels, {cal['particles']} particles, "
+                      f"{r['threads']} threads (SURVEY.md section 6 probe); the Euler ratio is applied to the pathline "
+                      "sample (the survey timed no reference pathline)"}
+
+
+def cpu_baseline(mesh, snap, back_snap, seeds, cells, args, n_steps, duration=None):
+    """The CPU oracle (port of the TBB path) on this host's cores, bounded sample; with the calibration
+    against the reference's own timings, the reference-equivalent rate beside it."""
     try:
         from oracle import oracle as O
     except Exception as e:  # pragma: no cover
         return {"error": f"oracle unavailable: {e}"}
+    duration = args.duration if duration is None else int(duration)
     threads = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or (os.cpu_count() or 1)
     threads = max(1, min(threads, os.cpu_count() or 1))
     derived = O.preprocess(mesh, snap)
     back = O.preprocess(mesh, back_snap) if back_snap is not None else None
     euler = args.method == "euler"
     # calibrate on a small sample, then size the timed sample to ~cpu_seconds
-    n0 = min(4000, len(seeds))
+    n0 = min(4000 if n_steps <= 20000 else 500, len(seeds))
     t = time.perf_counter()
-    O.run(mesh, derived, back, seeds[:n0], depth=args.depth, delta_t=args.dt, duration=args.duration,
+    O.run(mesh, derived, back, seeds[:n0], depth=args.depth, delta_t=args.dt, duration=duration,
           record_t=args.record, euler=euler, cells=cells[:n0], n_threads=threads, finalize=False)
     rate = n0 * n_steps / max(time.perf_counter() - t, 1e-6)
     n1 = int(min(len(seeds), max(n0, rate * args.cpu_seconds / n_steps)))
     t = time.perf_counter()
-    out = O.run(mesh, derived, back, seeds[:n1], depth=args.depth, delta_t=args.dt, duration=args.duration,
+    out = O.run(mesh, derived, back, seeds[:n1], depth=args.depth, delta_t=args.dt, duration=duration,
                 record_t=args.record, euler=euler, cells=cells[:n1], n_threads=threads, finalize=False)
     dt = time.perf_counter() - t
     death = out["death"].astype(np.int64)
     attempted = np.where(death < 0, n_steps, death + 1).sum()
-    return {"value": float(attempted / dt), "unit": "particle-steps/s", "cores": threads, "kind": "port",
-            "sample": f"{n1} of the same seeds x {n_steps} steps ({args.mode} {args.method}), same mesh/fields, "
-                      f"OpenMP schedule(dynamic,16) over particles; {dt:.1f} s"}
+    value = float(attempted / dt)
+    res = {"value": value, "unit": "particle-steps/s", "cores": threads, "kind": "port",
+           "sample": f"{n1} of the same seeds x {n_steps} steps ({'pathline' if back is not None else 'streamline'} "
+                     f"{args.method}, the first pair's snapshots), same mesh/fields, OpenMP schedule(dynamic,16) over "
+                     f"particles; {dt:.1f} s"}
+    cal = cpu_calibration(threads)
+    if cal is not None:
+        res["calibration"] = cal
+        res["reference_equivalent_value"] = value / cal["port_over_reference"]
+    return res
 
 
 if __name__ == "__main__":

@@ -11,7 +11,11 @@ with the MI355X-specific change that nothing leaves HBM between pairs:
 
 Per-pair semantics are the reference's:
 * pair p runs a PathLine with front = snapshot p, back = snapshot p+1 and
-  ``simulationDuration`` = the snapshot gap;
+  ``simulationDuration`` = that pair's snapshot gap, |t(p+1) - t(p)| from the
+  snapshots' timestamps (``_time_gap_seconds``, :1285-1295, :1444;
+  tutorial/pathLine.cpp:287-305) -- calendar-month pairs (28-31 days,
+  ``_month_pairs_forward/_backward``, :1236-1279) give every pair its own step
+  and record count;
 * seeds: pair 0 uses the given seeds, later pairs the previous pair's
   ``lastPoint`` if ``follow_last`` else the original seeds again (:1446-1459);
 * depth: constant mode re-applies ``cfg.depth`` every pair (``cfg.depth =
@@ -22,6 +26,8 @@ Per-pair semantics are the reference's:
 """
 from __future__ import annotations
 
+from datetime import datetime
+
 import numpy as np
 
 from . import _lib as L
@@ -29,12 +35,68 @@ from .engine import DeviceField, DeviceMesh, ParticleSet, TrajectoryConfig
 
 EARTH_RADIUS_M = 6_371_000.0  # pyMOPSAPI.py:46
 REORDER_SECONDS = 3 * 86400  # default launch length of long pairs (simulated time), see PathlineChain.run
+XTIME_FORMAT = "%Y-%m-%d_%H:%M:%S"  # MPAS xtime (pyMOPSAPI.py:1285; Utils.hpp:118)
+
+
+def month_pairs_forward(sy: int, sm: int, ey: int, em: int) -> list:
+    """(start, end) month pairs 'YYYY-MM-01' from (sy, sm) up to (ey, em), forward in time --
+    MOPSPathline._month_pairs_forward (tutorial/pyMOPSAPI.py:1236-1257; the C++ tutorial's
+    MOPS_IO::make_forward_month_pairs, YamlGen.hpp:360-379, yields the same list)."""
+    out = []
+    y, m = int(sy), int(sm)
+    while (y, m) <= (int(ey), int(em)):
+        ny, nm = (y + 1, 1) if m == 12 else (y, m + 1)
+        if (ny, nm) > (int(ey), int(em)):
+            break
+        out.append((f"{y:04d}-{m:02d}-01", f"{ny:04d}-{nm:02d}-01"))
+        y, m = ny, nm
+    return out
+
+
+def month_pairs_backward(sy: int, sm: int, ey: int, em: int) -> list:
+    """(start, end) month pairs from (sy, sm) back to (ey, em) -- MOPSPathline._month_pairs_backward
+    (tutorial/pyMOPSAPI.py:1259-1279)."""
+    out = []
+    y, m = int(sy), int(sm)
+    while (y, m) >= (int(ey), int(em)):
+        py_, pm = (y - 1, 12) if m == 1 else (y, m - 1)
+        if (py_, pm) < (int(ey), int(em)):
+            break
+        out.append((f"{y:04d}-{m:02d}-01", f"{py_:04d}-{pm:02d}-01"))
+        y, m = py_, pm
+    return out
+
+
+def time_gap_seconds(t1: str, t2: str, fmt: str = XTIME_FORMAT) -> int:
+    """t1 - t2 in seconds for MPAS timestamps, each cut at its first NUL and stripped
+    (MOPSPathline._time_gap_seconds, tutorial/pyMOPSAPI.py:1285-1295; C++ getTimeGapinSecond,
+    src/Utils/Utils.hpp:113-132)."""
+    a = datetime.strptime(t1.split("\x00", 1)[0].strip(), fmt)
+    b = datetime.strptime(t2.split("\x00", 1)[0].strip(), fmt)
+    return int((a - b).total_seconds())
+
+
+def pair_gaps(timestamps) -> list:
+    """Each consecutive snapshot pair's simulationDuration, |t(p+1) - t(p)| (pyMOPSAPI.py:1444)."""
+    ts = list(timestamps)
+    return [abs(time_gap_seconds(ts[p + 1], ts[p])) for p in range(len(ts) - 1)]
+
+
+def month_timestamps(pairs) -> list:
+    """The snapshot timestamps of a month-pair list: each pair's start, then the last pair's end
+    (the xtime of a monthly-mean file dated 'YYYY-MM-01', at 00:00:00)."""
+    if not pairs:
+        return []
+    return [a + "_00:00:00" for a, _ in pairs] + [pairs[-1][1] + "_00:00:00"]
 
 
 class PathlineChain:
-    def __init__(self, mesh: DeviceMesh, make_field, n_snapshots: int, gap_seconds: int, device=None,
-                 own_fields: bool = True, prefetch: bool = True, overlap_stream=None):
+    def __init__(self, mesh: DeviceMesh, make_field, n_snapshots: int, gap_seconds=None, device=None,
+                 own_fields: bool = True, prefetch: bool = True, overlap_stream=None, timestamps=None):
         """``make_field(i, stream) -> DeviceField`` builds snapshot i's field on ``stream``.
+        Pair p's simulationDuration: ``gap_seconds`` (one int for every pair, or a sequence with
+        one gap per pair), or from the snapshots' ``timestamps`` (MPAS xtime strings, one per
+        snapshot) as the reference computes it (``pair_gaps``).
         With ``own_fields`` False the fields are the caller's (e.g. all resident
         before a timed region) and are neither freed nor rebuilt here.
         ``prefetch`` builds snapshot p+2 on a side stream while pair p runs (3
@@ -54,7 +116,20 @@ class PathlineChain:
         self.mesh = mesh
         self.make_field = make_field
         self.n_snapshots = int(n_snapshots)
-        self.gap = int(gap_seconds)
+        if timestamps is not None:
+            if len(timestamps) != self.n_snapshots:
+                raise ValueError("one timestamp per snapshot")
+            gaps = pair_gaps(timestamps)
+        elif gap_seconds is None:
+            raise ValueError("give gap_seconds or timestamps")
+        elif np.isscalar(gap_seconds):
+            gaps = [int(gap_seconds)] * (self.n_snapshots - 1)
+        else:
+            gaps = [int(g) for g in gap_seconds]
+        if len(gaps) != self.n_snapshots - 1:
+            raise ValueError("one gap per snapshot pair")
+        self.gaps = gaps
+        self.gap = gaps[0]
         self.device = device
         self.own_fields = own_fields
         self.prefetch = prefetch
@@ -62,11 +137,13 @@ class PathlineChain:
 
     def run(self, seeds, depth: float, particle_depths=None, method: int = L.MOPS_EULER, delta_t: int = 60,
             record_t: int = 360, direction: int = L.MOPS_FORWARD, follow_last: bool = True, keep_lines: bool = True,
-            compute_stream=None, on_pair=None, timing=None, segment_steps: int = -1, reorder: bool = True):
+            compute_stream=None, on_pair=None, timing=None, segment_steps: int = -1, reorder: bool = True,
+            record_stride: int | None = None):
         """Run all pairs; returns device tensors {points, velocity, temperature,
         salinity, lastPoint, death_step (of the last pair)} when ``keep_lines``,
-        else only lastPoint/death_step.  ``on_pair(p, last)`` is called after pair p
-        is enqueued (timing / record gathers); ``timing`` (a list) receives an
+        else only lastPoint/death_step.  ``on_pair(p, last, ps)`` is called after pair p
+        is enqueued, with the pair's ParticleSet (its slot-ordered record slab, seeds and ids:
+        the multi-GPU record gather, distributed.RecordGather); ``timing`` (a list) receives an
         (start, end) HIP event pair around every trajectory launch.
         ``attempted`` in the result counts particle-steps whose velocity
         evaluation ran, summed over pairs (device scalar).  ``segment_steps``: integration
@@ -74,15 +151,23 @@ class PathlineChain:
         state and re-loads each particle's cell stencil; -1 = one launch per REORDER_SECONDS
         of simulated time).  ``reorder``: restore the particles' locality order between
         launches (long pairs: particles drift across many cells and a wave's lanes stop
-        sharing stencils -- config 5's 30-day pairs run 9% faster re-sorted every 3 days)."""
+        sharing stencils -- config 5's 30-day pairs run 9% faster re-sorted every 3 days).
+        ``record_stride``: columns of the record slab (default n; a multi-GPU shard pads it to the
+        largest shard so every rank's slab gathers with one all-gather)."""
         import torch
         dev = self.device or torch.device("cuda", torch.cuda.current_device())
         cs = compute_stream or torch.cuda.current_stream(dev)
         side = torch.cuda.Stream(device=dev)
-        cfg = TrajectoryConfig(deltaT=int(delta_t), simulationDuration=self.gap, recordT=int(record_t),
-                               depth=float(np.float32(depth)), direction=int(direction), method=int(method))
-        if cfg.n_steps <= 0 or cfg.n_records <= 0:
-            raise ValueError("invalid trajectory settings for a pair (deltaT/recordT vs the snapshot gap)")
+        cfgs = [TrajectoryConfig(deltaT=int(delta_t), simulationDuration=int(g), recordT=int(record_t),
+                                 depth=float(np.float32(depth)), direction=int(direction), method=int(method))
+                for g in self.gaps]
+        for c in cfgs:
+            if c.n_steps <= 0 or c.n_records <= 0:
+                raise ValueError("invalid trajectory settings for a pair (deltaT/recordT vs the snapshot gap "
+                                 f"{c.simulationDuration} s)")
+        # the particle set's record slab holds the longest pair's records; each pair runs with its own
+        # simulationDuration (steps, records, the alpha ramp)
+        cfg = max(cfgs, key=lambda c: c.n_records)
         # everything below is ordered on `cs` (the host never waits between pairs, so a
         # tensor touched on another stream could be read before `cs` has written it)
         with torch.cuda.stream(cs):
@@ -104,7 +189,7 @@ class PathlineChain:
             if overlap and self.n_snapshots > 2 and len(self.make_field.pool) < 1:
                 raise ValueError("overlap_stream needs a third field buffer in make_field.pool (seed the "
                                  "recycler with three fields and release them before the run)")
-            ps = ParticleSet(self.mesh, seeds0, cfg.depth, cfg, device=dev)
+            ps = ParticleSet(self.mesh, seeds0, cfg.depth, cfg, device=dev, record_stride=record_stride)
         period = ps.record_period(pathline=True)
         pts_acc, vel_acc, tmp_acc, sal_acc = [], [], [], []
         last = None
@@ -138,6 +223,8 @@ class PathlineChain:
                     d = pdep
                 else:
                     d = cfg.depth
+                cfg = cfgs[p]
+                ps.set_config(cfg)
                 # a continuation pair: each particle's current cell is an exact-locate hint
                 ps.reseed(s, d, stream=cs.cuda_stream, hint_cells=(p > 0 and follow_last))
                 front, back = fields[p], fields[p + 1]
@@ -164,7 +251,7 @@ class PathlineChain:
                     pts_acc.append(out["points"][:, sl]); vel_acc.append(out["velocity"][:, sl])
                     tmp_acc.append(out["temperature"][:, sl]); sal_acc.append(out["salinity"][:, sl])
             if on_pair is not None:
-                on_pair(p, last)
+                on_pair(p, last, ps)
             if overlap:
                 pair_done[p] = torch.cuda.Event()
                 pair_done[p].record(cs)  # snapshot p's buffer is free once pair p has run

@@ -94,3 +94,162 @@ def unshard_slots(gathered, gathered_ids, n_total: int, world: int):
     if seen != n_total:
         raise ValueError("shards do not cover n_total")
     return out
+
+
+def all_gather_flat(dist, out, inp, backend: str, group=None):
+    """One all-gather of a rank's flat slab into ``out`` ([world * inp.numel()]).  nccl (RCCL over
+    xGMI) runs on the caller's current stream; gloo (CPU tests, one-GPU rehearsals) stages device
+    tensors through host memory."""
+    if backend == "nccl" or not out.is_cuda:
+        dist.all_gather_into_tensor(out, inp, group=group)
+    else:
+        o = out.cpu()
+        dist.all_gather_into_tensor(o, inp.cpu(), group=group)
+        out.copy_(o)
+
+
+class RecordGather:
+    """The north star's trajectory collection: at every checkpoint -- the end of a
+    StreamLine call or of a chained pathline pair -- each rank's record slab is all-gathered, so
+    every rank holds the records of every particle.
+
+    A rank's ``ParticleSet`` keeps its records in slot (locality) order, so each checkpoint also
+    gathers, per slot, the run's seed (x, y, z) and the slot's particle id: with them
+    ``lines()`` rebuilds every line in global particle order (``unshard_slots`` +
+    ``mops_traj_finalize``), bit-identical to a single-rank run.
+
+    Overlap: ``collect`` swaps the particle set onto a second record slab (``ParticleSet.
+    swap_records``), so the next call writes one slab while the comm stream gathers the other; the
+    compute stream waits for a slab's gather only when that slab comes back a call later.  The
+    seeds and ids are copied into one of two aux buffers on the compute stream first (the next
+    call's reseed and re-sort rewrite them in place).
+
+    Bounded memory: a checkpoint's gathered records (world x K x 48 B per particle) can exceed what HBM
+    holds beside the fields (config 5 at 8 ranks: 149 GB per pair); with ``max_bytes`` the slab is
+    all-gathered in chunks of records through a ring of that size, in order on the comm stream, and
+    ``on_chunk(gathered, k0, k1)`` (enqueued on the comm stream before the next chunk overwrites the ring)
+    is where an output writer takes each chunk.
+
+    Torch device tensors (RCCL, or gloo staged through the host) and CPU tensors (gloo tests)."""
+
+    def __init__(self, dist, ps, world: int, backend: str = "nccl", comm_stream=None, group=None,
+                 max_bytes: int | None = None, on_chunk=None):
+        import torch
+        self.dist, self.world, self.backend, self.group = dist, int(world), backend, group
+        self.torch = torch
+        self.shape = tuple(ps.records.shape)            # [K_max][6][stride]
+        self.stride = self.shape[2]
+        dev = ps.records.device
+        self.cuda = ps.records.is_cuda
+        self.comm = comm_stream if (comm_stream is not None or not self.cuda) else torch.cuda.Stream(dev)
+        self.spare = torch.empty(self.shape, dtype=torch.float64, device=dev)
+        self.aux = [torch.zeros((4, self.stride), dtype=torch.float64, device=dev) for _ in range(2)]
+        per_rec = self.world * 6 * self.stride * 8
+        self.chunk = self.shape[0] if not max_bytes else max(1, min(self.shape[0], int(max_bytes) // per_rec))
+        self.on_chunk = on_chunk
+        self.gathered = torch.empty((self.world, self.chunk, 6, self.stride), dtype=torch.float64, device=dev)
+        self.gathered_aux = torch.empty((self.world, 4, self.stride), dtype=torch.float64, device=dev)
+        self._read = {}      # id(slab / aux) -> comm-stream event after the gather that read it
+        self._i = 0
+        self.K = 0            # records of the last gathered checkpoint
+        self.n = ps.n
+        self.done = None      # comm-stream event: the last checkpoint is in `gathered`
+        self.checkpoints = 0
+        self.bytes_per_rank = 0  # bytes each rank sent so far
+
+    def _wait(self, stream, key):
+        ev = self._read.pop(key, None)
+        if ev is not None and stream is not None:
+            stream.wait_event(ev)
+
+    def collect(self, ps, compute=None):
+        """Gather ``ps``'s current records (its first ``ps.K`` slots), seeds and slot ids; ``compute``:
+        the stream the particle set's work is ordered on (None: CPU)."""
+        torch = self.torch
+        if tuple(ps.records.shape) != self.shape:
+            raise ValueError("particle set record slab changed shape")
+        aux = self.aux[self._i]
+        self._i ^= 1
+        ctx = torch.cuda.stream(compute) if (self.cuda and compute is not None) else _null()
+        with ctx:
+            self._wait(compute, id(aux))  # its previous gather has read it
+            n = ps.n
+            aux[0:3, :n].copy_(ps.seeds.t())
+            aux[3, :n].copy_(ps.ids.to(torch.float64))
+            if n < self.stride:
+                aux[3, n:].fill_(-1.0)
+            slab = ps.records
+            self._wait(compute, id(self.spare))  # the slab about to be written again has been gathered
+            self.spare = ps.swap_records(self.spare)
+            ready = None
+            if self.cuda:
+                ready = torch.cuda.Event()
+                ready.record(compute if compute is not None else torch.cuda.current_stream(slab.device))
+        K = int(ps.K)
+        cctx = torch.cuda.stream(self.comm) if self.cuda else _null()
+        if self.cuda:
+            self.comm.wait_event(ready)
+        with cctx:
+            all_gather_flat(self.dist, self.gathered_aux.view(-1), aux.view(-1), self.backend, self.group)
+            row = 6 * self.stride
+            for k0 in range(0, K, self.chunk):
+                k1 = min(K, k0 + self.chunk)
+                m = (k1 - k0) * row
+                all_gather_flat(self.dist, self.gathered.view(-1)[: self.world * m],
+                                slab.view(-1)[k0 * row: k1 * row], self.backend, self.group)
+                if self.on_chunk is not None:
+                    self.on_chunk(self.gathered.view(-1)[: self.world * m].view(self.world, k1 - k0, 6, self.stride),
+                                  k0, k1)
+            if self.cuda:
+                ev = torch.cuda.Event()
+                ev.record(self.comm)
+                self._read[id(slab)] = ev
+                self._read[id(aux)] = ev
+                self.done = ev
+        self.K = K
+        self.checkpoints += 1
+        self.bytes_per_rank += (K * 6 + 4) * self.stride * 8
+        return self.done
+
+    def synchronize(self):
+        if self.cuda and self.comm is not None:
+            self.comm.synchronize()
+
+    def unsharded(self, n_total: int):
+        """(records [K][6][n_total], seeds [n_total][3]) of the last checkpoint in global particle
+        order (call after ``synchronize``; needs the whole slab in one chunk)."""
+        K, w = self.K, self.world
+        if K > self.chunk:
+            raise ValueError("the last checkpoint was gathered in chunks (max_bytes): take them in on_chunk")
+        g = self.gathered.view(-1)[: w * K * 6 * self.stride].view(w, K * 6, self.stride)
+        ids = self.gathered_aux[:, 3, :].to(self.torch.int64)
+        rec = unshard_slots(g, ids, n_total, w).view(K, 6, n_total)
+        seeds = unshard_slots(self.gathered_aux[:, 0:3, :], ids, n_total, w).t().contiguous()
+        return rec.contiguous(), seeds
+
+    def lines(self, n_total: int, pathline: bool, stream=None):
+        """Every particle's finalized line from the last checkpoint (device tensors; mops_traj_finalize
+        over the unsharded records, identity line order): what a single-rank run's finalize returns."""
+        import ctypes as C
+        from . import _lib as L
+        torch = self.torch
+        rec, seeds = self.unsharded(n_total)
+        K, P = self.K, self.K + 1
+        dev = rec.device
+        pts = torch.empty((n_total, P, 3), dtype=torch.float64, device=dev)
+        vel = torch.empty_like(pts)
+        tmp = torch.empty((n_total, P), dtype=torch.float64, device=dev)
+        sal = torch.empty_like(tmp)
+        last = torch.empty((n_total, 3), dtype=torch.float64, device=dev)
+        st = 0 if stream is None else int(stream.cuda_stream if hasattr(stream, "cuda_stream") else stream)
+        L.check(L.load().mops_traj_finalize(n_total, K, C.c_void_p(seeds.data_ptr()), C.c_void_p(rec.data_ptr()),
+                                            n_total, 1 if pathline else 0, None, C.c_void_p(pts.data_ptr()),
+                                            C.c_void_p(vel.data_ptr()), C.c_void_p(tmp.data_ptr()),
+                                            C.c_void_p(sal.data_ptr()), C.c_void_p(last.data_ptr()), C.c_void_p(st)),
+                "mops_traj_finalize")
+        return dict(points=pts, velocity=vel, temperature=tmp, salinity=sal, lastPoint=last)
+
+
+def _null():
+    import contextlib
+    return contextlib.nullcontext()

@@ -253,7 +253,10 @@ class ParticleSet:
     """
 
     def __init__(self, mesh: DeviceMesh, seeds_xyz, depth: float | np.ndarray, cfg: TrajectoryConfig, device=None,
-                 cells=None, use_order: bool = True):
+                 cells=None, use_order: bool = True, record_stride: int | None = None):
+        """``record_stride``: columns of the [K][6][stride] record slab (default n); a multi-GPU
+        shard pads it to the largest shard so every rank's slab has one shape
+        (distributed.RecordGather)."""
         import torch
         self.use_order = use_order
         self.torch = torch
@@ -279,7 +282,10 @@ class ParticleSet:
         else:
             self.cell = torch.as_tensor(np.asarray(cells, dtype=np.int32), device=dev).contiguous()
         self.K = cfg.n_records
-        self.records = torch.zeros((max(self.K, 1), 6, self.n), dtype=torch.float64, device=dev)
+        self.rec_stride = self.n if record_stride is None else int(record_stride)
+        if self.rec_stride < self.n:
+            raise ValueError("record_stride below the particle count")
+        self.records = torch.zeros((max(self.K, 1), 6, self.rec_stride), dtype=torch.float64, device=dev)
         self.order = torch.empty((self.n,), dtype=torch.int32, device=dev)
         # slot -> particle index: with use_order the state is kept PHYSICALLY in
         # locality order (state loads/stores and record stores coalesce);
@@ -324,7 +330,8 @@ class ParticleSet:
 
         def desc(src, dst, name, eb):
             if name == "records":
-                return L.PermArray(src.data_ptr() + 8 * lo, dst.data_ptr() + 8 * lo, 8, int(record_slots) * 6, self.n)
+                return L.PermArray(src.data_ptr() + 8 * lo, dst.data_ptr() + 8 * lo, 8, int(record_slots) * 6,
+                                   self.rec_stride)
             return L.PermArray(src.data_ptr() + eb * lo, dst.data_ptr() + eb * lo, eb, 1, n)
 
         lib = L.load()
@@ -382,9 +389,26 @@ class ParticleSet:
                 "mops_order_particles_live")
         kw = min(int(records_written), self.records.shape[0])
         self._apply_order(self.order, lo, hi, s, kw)
-        L.check(lib.mops_records_clear_dead(n, C.c_void_p(self._n_live[key].data_ptr()), kw, self.records.shape[0],
-                                            C.c_void_p(self.records.data_ptr() + 8 * lo), self.n,
+        L.check(lib.mops_records_clear_dead(n, C.c_void_p(self._n_live[key].data_ptr()), kw, self.K,
+                                            C.c_void_p(self.records.data_ptr() + 8 * lo), self.rec_stride,
                                             _stream_handle(s)), "mops_records_clear_dead")
+
+    def set_config(self, cfg: TrajectoryConfig):
+        """Run the next call with ``cfg`` (a chained pair's own simulationDuration: its step and
+        record counts and alpha ramp); its records must fit the slab allocated at creation."""
+        if cfg.n_records > self.records.shape[0]:
+            raise ValueError(f"{cfg.n_records} records do not fit the slab of {self.records.shape[0]}")
+        self.cfg = cfg
+        self._c = cfg.ctype()
+        self.K = cfg.n_records
+
+    def swap_records(self, slab):
+        """Install another [K][6][stride] slab as the record buffer and return the current one
+        (RecordGather: the slab just completed is gathered while the next call writes this one)."""
+        if tuple(slab.shape) != tuple(self.records.shape) or slab.dtype != self.records.dtype:
+            raise ValueError("record slab shape/dtype mismatch")
+        old, self.records = self.records, slab
+        return old
 
     def reset(self, depth=None):
         self.x.copy_(self.seeds[:, 0]); self.y.copy_(self.seeds[:, 1]); self.z.copy_(self.seeds[:, 2])
@@ -427,7 +451,7 @@ class ParticleSet:
         p = self.particles()
         st = L.load().mops_traj_advance(self.mesh.handle, front.handle, None if back is None else back.handle,
                                         C.byref(self._c), C.byref(p), int(step_begin), int(step_end),
-                                        C.c_void_p(self.records.data_ptr()), self.n, _stream_handle(stream))
+                                        C.c_void_p(self.records.data_ptr()), self.rec_stride, _stream_handle(stream))
         L.check(st, "mops_traj_advance")
         self._written = True
 
@@ -493,7 +517,7 @@ class ParticleSet:
                 p = self._sub_particles(lo, hi, self._n_live.get((lo, hi)) if (compact and t > 0) else None)
                 rc = lib.mops_traj_advance(self.mesh.handle, front.handle, None if back is None else back.handle,
                                            C.byref(self._c), C.byref(p), tb[t], tb[t + 1],
-                                           C.c_void_p(self.records.data_ptr() + 8 * lo), self.n,
+                                           C.c_void_p(self.records.data_ptr() + 8 * lo), self.rec_stride,
                                            _stream_handle(st))
                 L.check(rc, "mops_traj_advance")
                 if timing is not None:
@@ -546,7 +570,8 @@ class ParticleSet:
                 e0.record(ts)
             # a part's slots write the lines ids[slot] of the full outputs
             rc = lib.mops_traj_finalize(hi - lo, self.K, C.c_void_p(self.seeds.data_ptr() + 24 * lo),
-                                        C.c_void_p(self.records.data_ptr() + 8 * lo), self.n, 1 if pathline else 0,
+                                        C.c_void_p(self.records.data_ptr() + 8 * lo), self.rec_stride,
+                                        1 if pathline else 0,
                                         C.c_void_p(self.ids.data_ptr() + 4 * lo), C.c_void_p(pts.data_ptr()),
                                         C.c_void_p(vel.data_ptr()), C.c_void_p(tmp.data_ptr()),
                                         C.c_void_p(sal.data_ptr()), C.c_void_p(last.data_ptr()), _stream_handle(st))

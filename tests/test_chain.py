@@ -9,18 +9,20 @@ EARTH_RADIUS_M = 6_371_000.0
 def oracle_chain(O, mesh, snaps, seeds, depth, particle_depths, gap, dt, rT, euler, follow_last=True,
                  derived=None):
     """MOPSPathline.run semantics on the oracle; ``derived`` (oracle.Derived per snapshot) replaces
-    the host preprocessing of ``snaps`` (e.g. fields exported from HBM at oRRS18to6 size)."""
+    the host preprocessing of ``snaps`` (e.g. fields exported from HBM at oRRS18to6 size); ``gap``:
+    one simulationDuration for every pair or one per pair (pyMOPSAPI.py:1444)."""
     if derived is None:
         derived = [O.preprocess(mesh, s) for s in snaps]
     snaps = derived
     pts, vel, tmp, sal = [], [], [], []
     last = None
     pdep = None if particle_depths is None else np.asarray(particle_depths, dtype=np.float32)
+    gaps = [gap] * (len(snaps) - 1) if np.isscalar(gap) else list(gap)
     for p in range(len(snaps) - 1):
         s = seeds if (p == 0 or not follow_last) else last
         if pdep is not None and p > 0 and follow_last:
             pdep = np.clip(EARTH_RADIUS_M - np.linalg.norm(s, axis=1), 0.0, None).astype(np.float32)
-        r = O.run(mesh, derived[p], derived[p + 1], s, depth=depth, depths=pdep, delta_t=dt, duration=gap,
+        r = O.run(mesh, derived[p], derived[p + 1], s, depth=depth, depths=pdep, delta_t=dt, duration=gaps[p],
                   record_t=rT, euler=euler)
         sl = slice(None) if p == 0 else slice(1, None)
         pts.append(r["points"][:, sl]); vel.append(r["velocity"][:, sl])
@@ -46,6 +48,30 @@ def test_chain_matches_oracle(engine_lib, oracle_lib, gpu, small_case, method, p
     got = chain.run(seeds, depth=300.0, particle_depths=pd, method=method, delta_t=600, record_t=3600)
     ref = oracle_chain(oracle_lib, mesh, snaps, seeds, 300.0, pd, 21600, 600, 3600, euler=(method == 1))
     assert got["points"].shape[1] == 7 + 6          # 6 records + seed, then 6 more records
+    for k in ("points", "velocity", "temperature", "salinity", "lastPoint"):
+        assert np.array_equal(got[k].cpu().numpy(), ref[k]), k
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("method", [1, 0], ids=["euler", "rk4"])
+def test_chain_unequal_gaps_from_timestamps(engine_lib, oracle_lib, gpu, small_case, method):
+    """Per-pair simulationDuration from the snapshots' timestamps (pyMOPSAPI.py:1444, _time_gap_seconds
+    :1285-1295): pairs of 6 h, 2 h and 4 h -- different step and record counts and alpha ramps per pair
+    -- bit-exact against the oracle chain run with the same gaps."""
+    from mops_amd import synth
+    from mops_amd.chain import PathlineChain, pair_gaps, snapshot_field_factory
+    from mops_amd.engine import DeviceMesh
+    mesh, _, _ = small_case
+    ts = ["0001-01-01_00:00:00", "0001-01-01_06:00:00", "0001-01-01_08:00:00", "0001-01-01_12:00:00"]
+    gaps = pair_gaps(ts)
+    assert gaps == [21600, 7200, 14400]
+    snaps = [synth.make_snapshot(mesh, timestep=t, phase=0.35 * t) for t in range(len(ts))]
+    seeds = synth.uniform_band_seeds(150, seed=12)
+    dm = DeviceMesh.from_mesh(mesh)
+    chain = PathlineChain(dm, snapshot_field_factory(dm, lambda i: snaps[i]), len(snaps), timestamps=ts)
+    got = chain.run(seeds, depth=300.0, method=method, delta_t=600, record_t=3600)
+    ref = oracle_chain(oracle_lib, mesh, snaps, seeds, 300.0, None, gaps, 600, 3600, euler=(method == 1))
+    assert got["points"].shape[1] == 1 + 6 + 2 + 4
     for k in ("points", "velocity", "temperature", "salinity", "lastPoint"):
         assert np.array_equal(got[k].cpu().numpy(), ref[k]), k
 

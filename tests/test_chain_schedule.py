@@ -1,0 +1,178 @@
+"""CPU tests of the chain's pair schedule (calendar-month pairs, per-pair gaps from timestamps),
+the bench's default workload, and the multi-GPU record collection (distributed.RecordGather)
+over gloo with world size 2.
+
+The month-pair and time-gap vectors are the reference's own functions' outputs
+(tests/golden/month_pairs.json, made by tests/golden/make_month_pairs.py from
+tutorial/pyMOPSAPI.py:1236-1295)."""
+import json
+import os
+import sys
+
+import numpy as np
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+GOLD = os.path.join(ROOT, "tests", "golden", "month_pairs.json")
+
+
+def test_month_pairs_match_reference_vectors():
+    from mops_amd import chain
+    g = json.load(open(GOLD))
+    for case in g["forward"]:
+        assert [list(p) for p in chain.month_pairs_forward(*case["args"])] == case["pairs"], case["args"]
+    for case in g["backward"]:
+        assert [list(p) for p in chain.month_pairs_backward(*case["args"])] == case["pairs"], case["args"]
+
+
+def test_time_gaps_match_reference_vectors():
+    from mops_amd import chain
+    g = json.load(open(GOLD))
+    assert len(g["gaps"]) > 100
+    for case in g["gaps"]:
+        assert chain.time_gap_seconds(case["t1"], case["t2"]) == case["seconds"], (case["t1"], case["t2"])
+
+
+def test_calendar_year_schedule():
+    """Config 5's schedule: 12 calendar-month pairs from January = 365 days = 525 600 steps at dt 60."""
+    from mops_amd import chain
+    pairs = chain.month_pairs_forward(1, 1, 2, 1)
+    ts = chain.month_timestamps(pairs)
+    gaps = chain.pair_gaps(ts)
+    assert len(pairs) == 12 and len(ts) == 13
+    assert [g // 86400 for g in gaps] == [31, 28, 31, 30, 31, 30, 31, 31, 30, 31, 30, 31]
+    assert sum(gaps) // 60 == 525_600
+    # backward: the same months in reverse, |gap| (pyMOPSAPI.py:1444 takes abs)
+    back = chain.month_pairs_backward(2, 1, 1, 1)
+    assert chain.pair_gaps(chain.month_timestamps(back)) == gaps[::-1]
+
+
+def test_chain_accepts_per_pair_gaps_and_timestamps():
+    from mops_amd.chain import PathlineChain
+    ts = ["0001-01-01_00:00:00", "0001-02-01_00:00:00", "0001-03-01_00:00:00"]
+    c = PathlineChain(None, None, 3, timestamps=ts)
+    assert c.gaps == [31 * 86400, 28 * 86400]
+    assert PathlineChain(None, None, 3, gap_seconds=[100, 200]).gaps == [100, 200]
+    assert PathlineChain(None, None, 4, gap_seconds=600).gaps == [600] * 3
+    with pytest.raises(ValueError):
+        PathlineChain(None, None, 3, gap_seconds=[1, 2, 3])
+    with pytest.raises(ValueError):
+        PathlineChain(None, None, 3, timestamps=ts[:2])
+
+
+def _bench():
+    import importlib.util
+    spec = importlib.util.spec_from_file_location("bench_under_test", os.path.join(ROOT, "bench.py"))
+    b = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(b)
+    return b
+
+
+def test_bench_default_is_config3():
+    """`python bench.py` (the driver's command) runs BASELINE config 3, the largest single-GPU config:
+    1e7 particles, layer 10, dt 60 s, 7 daily pairs; config 5 runs the calendar year."""
+    b = _bench()
+    a = b.apply_config_defaults(b.parse(["--steps", "20", "--warmup", "5"]))
+    assert (a.config, a.particles, a.dt, a.pairs, a.mode, a.method) == (3, 10_000_000, 60, 7, "pathline", "euler")
+    assert (a.steps, a.warmup) == (20, 5)
+    a = b.apply_config_defaults(b.parse([]))
+    assert a.config == 3 and (a.steps, a.warmup) == (3, 1) and a.gather == "records"
+    from mops_amd import chain
+    assert chain.pair_gaps(b.chain_timestamps(3, 7)) == [86400] * 7
+    a5 = b.apply_config_defaults(b.parse(["--config", "5"]))
+    assert a5.pairs == 12 and a5.record == 86400 and (a5.steps, a5.warmup) == (1, 0)
+    g5 = chain.pair_gaps(b.chain_timestamps(5, a5.pairs))
+    assert sum(g // a5.dt for g in g5) == 525_600 and all(g % a5.record == 0 for g in g5)
+    a2 = b.apply_config_defaults(b.parse(["--config", "2"]))
+    assert (a2.particles, a2.dt, a2.mode) == (1_000_000, 120, "streamline")
+
+
+class _Shard:
+    """The parts of a ParticleSet that RecordGather reads: slot-ordered records, seeds and ids."""
+
+    def __init__(self, records, seeds, ids, K):
+        self.records, self.seeds, self.ids, self.K, self.n = records, seeds, ids, K, seeds.shape[0]
+
+    def swap_records(self, slab):
+        old, self.records = self.records, slab
+        return old
+
+
+def _gather_worker(rank, world, port, q):
+    import torch
+    import torch.distributed as dist
+    from oracle import oracle as O
+    from mops_amd import synth
+    from mops_amd.distributed import RecordGather, max_shard, shard_bounds
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        mesh = synth.make_mesh(12, n_levels=8)
+        snaps = [synth.make_snapshot(mesh, timestep=t, phase=0.35 * t) for t in range(3)]
+        d = [O.preprocess(mesh, s) for s in snaps]
+        seeds = synth.uniform_band_seeds(91, seed=5)
+        n_total = len(seeds)
+        lo, hi = shard_bounds(n_total, rank, world)
+        npad = max_shard(n_total, world)
+        gaps = [14400, 7200]  # two chained pairs of different length: K = 4, then 2 records
+        rng = np.random.default_rng(100 + rank)
+        kmax = max(gaps) // 3600
+        ok = True
+        coll = None
+        s_all = seeds
+        for p, gap in enumerate(gaps):
+            ref = O.run(mesh, d[p], d[p + 1], s_all, depth=200.0, delta_t=600, duration=gap, record_t=3600,
+                        n_threads=1, finalize=False)
+            K = gap // 3600
+            # this rank's shard in a random slot order, as ParticleSet keeps it
+            perm = rng.permutation(hi - lo)
+            rec = torch.zeros((kmax, 6, npad), dtype=torch.float64)
+            rec[:K, 0:3, : hi - lo] = torch.as_tensor(ref["rec_pos"][lo:hi][perm].transpose(1, 2, 0))
+            rec[:K, 3:6, : hi - lo] = torch.as_tensor(ref["rec_vel"][lo:hi][perm].transpose(1, 2, 0))
+            sd = torch.as_tensor(np.ascontiguousarray(s_all[lo:hi][perm]))
+            ids = torch.as_tensor(perm.astype(np.int32))
+            shard = _Shard(rec, sd, ids, K)
+            if coll is None:
+                coll = RecordGather(dist, shard, world, backend="gloo")
+            coll.collect(shard)
+            got_rec, got_seeds = coll.unsharded(n_total)
+            ok &= np.array_equal(got_rec[:, 0:3].numpy().transpose(2, 0, 1), ref["rec_pos"])
+            ok &= np.array_equal(got_rec[:, 3:6].numpy().transpose(2, 0, 1), ref["rec_vel"])
+            ok &= np.array_equal(got_seeds.numpy(), s_all)
+            ok &= shard.records is not rec  # the particle set moved to the spare slab
+            s_all = np.ascontiguousarray(ref["rec_pos"][:, K - 1])  # continuation points
+        # bounded ring: the last checkpoint again, gathered in chunks of one record through on_chunk
+        chunks = []
+        shard2 = _Shard(rec.clone(), sd, ids, K)
+        ring = RecordGather(dist, shard2, world, backend="gloo", max_bytes=world * 6 * npad * 8,
+                            on_chunk=lambda g, k0, k1: chunks.append((k0, k1, g.clone())))
+        ring.collect(shard2)
+        ok &= ring.chunk == 1 and [c[:2] for c in chunks] == [(0, 1), (1, 2)]
+        whole = coll.gathered.view(-1)[: world * K * 6 * npad].view(world, K, 6, npad)
+        ok &= torch.equal(torch.cat([c[2] for c in chunks], 1), whole)
+        q.put((rank, bool(ok)))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_record_gather_gloo_world2_chain_shaped():
+    """Two chained pairs with different record counts: each rank's slot-ordered records, gathered by
+    RecordGather and unsharded by the slot ids, equal the single-process (oracle) records bit for bit."""
+    import multiprocessing as mp
+    import socket
+    from oracle import oracle as O
+    O.build()
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    procs = [ctx.Process(target=_gather_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    for p in procs:
+        p.join(timeout=240)
+    assert all(p.exitcode == 0 for p in procs)
+    res = dict(q.get(timeout=5) for _ in range(2))
+    assert res == {0: True, 1: True}
