@@ -91,6 +91,30 @@ constexpr int kNrmSlots(int maxv) { return (MOPS_LDS_COMPACT && maxv > MOPS_NRM_
 
 inline int rec_ints_for(int maxv) { return ((1 + 2 * maxv) + 3) / 4 * 4; }
 
+// Cooperative waves (pathline Euler, MAXV 7): the pathline kernel is bound by the texture-data
+// unit that returns VMEM data to the lanes (TD 96-98% busy at configs 3/4), because every lane
+// gathers its own 12 level-pair records and 7 polygon slots although a wave's lanes share one to
+// three cells.  A wave whose live lanes form at most MOPS_COOP_G groups of equal (cell, hinted
+// front layer, hinted back layer) loads each group's polygon and records ONCE -- one 16-B piece
+// per lane, the pieces of all groups spread over the wave -- into an LDS tile, and its lanes
+// read them from there (ds_read_b128).  Same doubles, same order: bit-identical results.
+#ifndef MOPS_COOP_PE
+#define MOPS_COOP_PE 1
+#endif
+#ifndef MOPS_GR_COOP
+#define MOPS_GR_COOP 1  // level-pair records per LDS round trip in the tile instantiations
+#endif
+#ifndef MOPS_COOP_R
+#define MOPS_COOP_R 4  // tile pieces per live lane at most (fewer live lanes: the lanes gather themselves)
+#endif
+#ifndef MOPS_COOP_G
+#define MOPS_COOP_G 2  // groups per wave with a tile (LDS: 1344 B + a 48-B header each)
+#endif
+constexpr int kTilePoly = 2 * 7;           // 16-B pieces: 7 packed polygon slots {x, y, z, B_j}
+constexpr int kTileRec = (kPairRec / 2) * 7;  // 7 level-pair records of one field
+constexpr int kTilePieces = kTilePoly + 2 * kTileRec;  // 84 pieces = 1344 B per group
+constexpr int kTileHdr = 12;               // ints per group header: nv, cell, h0, h1, vid[7], pad
+
 }  // namespace
 
 struct mops_mesh {
@@ -606,9 +630,9 @@ __device__ __forceinline__ int nverts(const Cell<MAXV>& c) { return NV > 0 ? NV 
 
 // guards + TBBKernel::IsInMesh + Interpolator::CalcPolygonWachspress
 // (MPASOVisualizerKernels.cpp:744-770, TBBKernel.h:21-54, Interpolation.hpp:137-165)
-template <int MAXV, int NV>
+template <int MAXV, int NV, bool COOP = false>
 __device__ __forceinline__ bool weights(const Cell<MAXV>& c, int L, int V, double px, double py, double pz,
-                                        double* w) {
+                                        double* w, const double4* tpoly = nullptr) {
     if (c.id < 0 || L <= 1 || L > kMaxLevels) return false;
     const int nv = nverts<NV>(c);
     if (nv <= 0 || nv > kMaxVertex) return false;
@@ -622,8 +646,11 @@ __device__ __forceinline__ bool weights(const Cell<MAXV>& c, int L, int V, doubl
         } else {
             if (j < nv) {
 #if MOPS_CPOLY
-                // one 32-B slot {x, y, z, B_j} of the cell's packed polygon: 2 VMEM instead of 3
-                const double4 q = c.cpoly[(int64_t)c.id * MAXV + j];
+                // one 32-B slot {x, y, z, B_j} of the cell's packed polygon: 2 VMEM instead of 3; in a
+                // cooperative wave (coop, wave-uniform) the same slot from the wave's LDS tile
+                double4 q;
+                if constexpr (COOP) q = tpoly[j];
+                else q = c.cpoly[(int64_t)c.id * MAXV + j];
                 X[j] = q.x; Y[j] = q.y; Z[j] = q.z; BB[j] = q.w;
 #else
                 const double4 q = c.vxyz[j == 0 ? c.vlast : c.vid[(j + MAXV - 1) % MAXV]];
@@ -1086,20 +1113,22 @@ struct Pair {
 #ifndef MOPS_PAIR_BARRIER
 #define MOPS_PAIR_BARRIER 1
 #endif
-template <int MAXV, int GR, int NV>
+template <int MAXV, int GR, int NV, bool COOP = false>
 __device__ __forceinline__ void pair_sums(const Cell<MAXV>& c, const double* w, const double* __restrict__ pr, int L,
-                                          int k, Pair& S) {
+                                          int k, Pair& S, const double2* trec = nullptr) {
     MOPS_MARK(300 + NV);
     S.zm = S.zk = S.wm = S.wk = 0.0;
     S.um0 = S.um1 = S.um2 = S.uk0 = S.uk1 = S.uk2 = 0.0;
     // 32-bit record indices: V * L < 2^31 (mops_mesh_create), so v*(L-1) + k - 1 fits
     const uint32_t zrec = (uint32_t)c.V * (uint32_t)(L - 1);
+    // tile reads (LDS latency) need fewer records in flight than gathers
+    constexpr int GR_ = COOP ? MOPS_GR_COOP : GR;
 #pragma unroll
-    for (int v0 = 0; v0 < MAXV; v0 += GR) {
+    for (int v0 = 0; v0 < MAXV; v0 += GR_) {
         if (v0 < nverts<NV>(c)) {
-            double2 a[GR][kPairRec / 2];
+            double2 a[GR_][kPairRec / 2];
 #pragma unroll
-            for (int j = 0; j < GR; ++j) {
+            for (int j = 0; j < GR_; ++j) {
                 const int v = v0 + j;
                 if (v >= MAXV) break;
     #if defined(MOPS_ABL_PAIR1)
@@ -1111,12 +1140,17 @@ __device__ __forceinline__ void pair_sums(const Cell<MAXV>& c, const double* w, 
             const uint32_t ri = (v < nverts<NV>(c)) ? (uint32_t)c.vid[v] * (uint32_t)(L - 1) + (uint32_t)(k - 1) : zrec;
 #endif
 #endif
-                const double2* r = reinterpret_cast<const double2*>(pr + (uint64_t)ri * kPairRec);
+                if constexpr (COOP) {  // the wave's LDS tile: this vertex's record at the group's layer (zeros past nv)
 #pragma unroll
-                for (int q = 0; q < kPairRec / 2; ++q) a[j][q] = r[q];
+                    for (int q = 0; q < kPairRec / 2; ++q) a[j][q] = trec[(kPairRec / 2) * v + q];
+                } else {
+                    const double2* r = reinterpret_cast<const double2*>(pr + (uint64_t)ri * kPairRec);
+#pragma unroll
+                    for (int q = 0; q < kPairRec / 2; ++q) a[j][q] = r[q];
+                }
             }
 #pragma unroll
-            for (int j = 0; j < GR; ++j) {
+            for (int j = 0; j < GR_; ++j) {
                 const int v = v0 + j;
                 if (v >= MAXV) break;
                 const double wv = w[v];
@@ -1127,7 +1161,7 @@ __device__ __forceinline__ void pair_sums(const Cell<MAXV>& c, const double* w, 
             }
             // NV > 0 has no per-group branch: keep the groups apart, or the
             // scheduler puts every record in flight at once and spills
-            if constexpr (NV > 0 && MOPS_PAIR_BARRIER) __builtin_amdgcn_sched_barrier(0);
+            if constexpr ((NV > 0 || COOP) && MOPS_PAIR_BARRIER) __builtin_amdgcn_sched_barrier(0);
         }
     }
     MOPS_MARK(310 + NV);
@@ -1147,13 +1181,14 @@ __device__ __forceinline__ void pair_sums(const Cell<MAXV>& c, const double* w, 
 // bottom" branch).  Otherwise bracket_mono walks from the hint inside the prefix,
 // and bracket_scan (the whole fixed-up column) runs when the walk would leave
 // it; the record of the final layer is then read.
-template <int MAXV, bool PATH, int GR, int NV>
+template <int MAXV, bool PATH, int GR, int NV, bool COOP = false>
 __device__ __forceinline__ int layer_eval(const Cell<MAXV>& c, const double* w, int km, const Field& f, int L,
-                                          double d, int& hint, Pair& S) {
+                                          double d, int& hint, Pair& S, const double2* trec = nullptr) {
     const double eps = 1e-8;
     const int h = hint;
     if (h >= 1 && h <= km) {  // km = -1: general bracket only (fast_ok)
-        pair_sums<MAXV, GR, NV>(c, w, f.pr, L, h, S);
+        // (a cooperative wave's tile holds every vertex's record at exactly this hinted layer)
+        pair_sums<MAXV, GR, NV, COOP>(c, w, f.pr, L, h, S, trec);
         bool ok;
         if (h == 1 && d > S.zm + eps) {  // above the surface (z_0 = z_{h-1} here)
             ok = true;
@@ -1219,16 +1254,19 @@ __device__ __forceinline__ bool eval_stream(const Cell<MAXV>& c, int L, int V, c
 // pathline calc_velocity_at (MPASOVisualizerKernels.cpp:1124-1327).  The
 // attribute channel is not evaluated: FinalizeTrajectoryLinesWithAttrs never
 // reads it (TrajectoryCommon.h:176-185, quirk Q9), so it is unobservable.
-template <int MAXV, int GR, int NV>
+template <int MAXV, int GR, int NV, bool COOP = false>
 __device__ __forceinline__ bool eval_path(const Cell<MAXV>& c, int L, int V, const Field& ff, const Field& fb,
                                           double px, double py, double pz, double d, double alpha, int& hint0,
-                                          int& hint1, double& hx, double& hy, double& hz, double& wv) {
+                                          int& hint1, double& hx, double& hy, double& hz, double& wv,
+                                          const double2* tile = nullptr) {
     double w[MAXV];
-    if (!weights<MAXV, NV>(c, L, V, px, py, pz, w)) return false;
+    if (!weights<MAXV, NV, COOP>(c, L, V, px, py, pz, w, reinterpret_cast<const double4*>(tile))) return false;
     const bool wfin = weights_finite<MAXV, NV>(c, w);
     Pair F, B;
-    const int lf = layer_eval<MAXV, true, GR, MOPS_HEX_PAIRS_P ? NV : 0>(c, w, fast_ok<MAXV, NV>(c, c.mono0, wfin, w), ff, L, d, hint0, F);
-    const int lb = layer_eval<MAXV, true, GR, MOPS_HEX_PAIRS_P ? NV : 0>(c, w, fast_ok<MAXV, NV>(c, c.mono1, wfin, w), fb, L, d, hint1, B);
+    const int lf = layer_eval<MAXV, true, GR, MOPS_HEX_PAIRS_P ? NV : 0, COOP>(c, w, fast_ok<MAXV, NV>(c, c.mono0, wfin, w), ff, L, d, hint0, F,
+                                                                               tile + kTilePoly);
+    const int lb = layer_eval<MAXV, true, GR, MOPS_HEX_PAIRS_P ? NV : 0, COOP>(c, w, fast_ok<MAXV, NV>(c, c.mono1, wfin, w), fb, L, d, hint1, B,
+                                                                               tile + kTilePoly + kTileRec);
     if (lf < 0 || lb < 0) return false;
     const double xf = dmax(F.zk, dmin(d, F.zm));
     const double denf = F.zm - F.zk;
@@ -1257,7 +1295,16 @@ __device__ __forceinline__ bool eval_path(const Cell<MAXV>& c, int L, int V, con
 template <int MAXV, bool PATH, int GR>
 __device__ __forceinline__ bool eval_at(bool hex, const Cell<MAXV>& c, int L, int V, const Field& f0,
                                         const Field& f1, double px, double py, double pz, double d, double alpha,
-                                        int& hint0, int& hint1, double& hx, double& hy, double& hz, double& wv) {
+                                        int& hint0, int& hint1, double& hx, double& hy, double& hz, double& wv,
+                                        bool coop = false, const double2* tile = nullptr) {
+    if constexpr (MAXV == 7 && PATH) {
+        if (coop) {  // wave-uniform: the tile instantiations
+            if (hex) return eval_path<MAXV, GR, 6, true>(c, L, V, f0, f1, px, py, pz, d, alpha, hint0, hint1, hx, hy,
+                                                         hz, wv, tile);
+            return eval_path<MAXV, GR, 0, true>(c, L, V, f0, f1, px, py, pz, d, alpha, hint0, hint1, hx, hy, hz, wv,
+                                                tile);
+        }
+    }
     if constexpr (MAXV == 7) {
         if (hex)
             return PATH ? eval_path<MAXV, GR, 6>(c, L, V, f0, f1, px, py, pz, d, alpha, hint0, hint1, hx, hy, hz, wv)
@@ -1418,6 +1465,10 @@ __global__ void __launch_bounds__(kTrajBlock, (TrajWaves<MAXV, PATH, EULER>::val
     __shared__ float s_rb2[kPairT && MOPS_LDS_COMPACT ? kTrajBlock : 1];
     c.pr2 = s_pr2 + threadIdx.x;
     c.rb2 = s_rb2 + (kPairT && MOPS_LDS_COMPACT ? threadIdx.x : 0);
+    // cooperative waves (see kTilePieces): the wave's LDS tile and its group headers
+    constexpr bool kCoop = PATH && EULER && MAXV == 7 && !kRC && MOPS_CPOLY && MOPS_COOP_PE;
+    __shared__ double2 s_tile[kCoop ? MOPS_COOP_G * kTilePieces : 1];
+    __shared__ int4 s_hdr[kCoop ? MOPS_COOP_G * (kTileHdr / 4) : 1];
     const int C = a.C;
     // next recording step (the smallest j >= step_begin with (j+1) % rec_period == 0) and its
     // record index, advanced by counting instead of a 64-bit modulo per step
@@ -1503,11 +1554,82 @@ __global__ void __launch_bounds__(kTrajBlock, (TrajWaves<MAXV, PATH, EULER>::val
         const double d = -1.0 * (double)dep;
         const double r = dev::len3(x, y, z);
         const bool hex = MOPS_HEX && __all(c.nv == 6);  // wave-uniform (dev::eval_at)
+        bool coop = false;  // wave-uniform: this step's polygon and hinted-layer records come from s_tile
+        const double2* tile = nullptr;
+        if constexpr (kCoop) {
+            // groups of live lanes with equal (cell, hint0, hint1), found leader by leader with
+            // scalar readlanes + ballots; more than MOPS_COOP_G groups: the lanes gather themselves
+            const uint64_t act = __ballot(1);
+            uint64_t rem = act;
+            int g = 0, G = 0;
+            bool lead = false;
+            while (rem != 0ull && G < MOPS_COOP_G) {
+                const int ld = __builtin_ctzll(rem);
+                const int kc = __builtin_amdgcn_readlane(cell, ld);
+                const int k0 = __builtin_amdgcn_readlane(hint0, ld);
+                const int k1 = __builtin_amdgcn_readlane(hint1, ld);
+                const bool mine = (cell == kc) & (hint0 == k0) & (hint1 == k1);
+                const uint64_t m = __ballot(mine);
+                if (mine) g = G;
+                lead |= ((int)__lane_id() == ld);
+                rem &= ~m;
+                ++G;
+            }
+            // the pieces are spread over the live lanes only (a dead or finished lane has left the
+            // loop): at most MOPS_COOP_R per lane
+            const int nact = __popcll(act);
+            coop = rem == 0ull && G * kTilePieces <= MOPS_COOP_R * nact;
+            if (coop) {
+                if (lead) {  // the group's header: {nv, cell, h0, h1}, vid[0..3], vid[4..6]
+                    int4* hd = s_hdr + g * (kTileHdr / 4);
+                    hd[0] = make_int4(c.nv, cell, hint0, hint1);
+                    hd[1] = make_int4(c.vid[0], c.vid[1], c.vid[2], c.vid[3]);
+                    hd[2] = make_int4(c.vid[4], c.vid[5], c.vid[6], 0);
+                }
+                __builtin_amdgcn_wave_barrier();  // (one wave per block: its LDS operations run in order)
+                const int np = G * kTilePieces;
+                const uint32_t zrec = (uint32_t)a.V * (uint32_t)(a.L - 1);
+                const int* hdi = reinterpret_cast<const int*>(s_hdr);
+                // this lane's rank among the live lanes
+                const int rank = (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(act >> 32),
+                                                                __builtin_amdgcn_mbcnt_lo((uint32_t)act, 0u));
+#pragma unroll
+                for (int rr = 0; rr < MOPS_COOP_R; ++rr) {
+                    const int i = rank + nact * rr;
+                    if (i < np) {
+                        const int gg = i / kTilePieces, pc = i - gg * kTilePieces;
+                        const int4 h4 = s_hdr[gg * (kTileHdr / 4)];
+                        const double2* src;
+                        if (pc < kTilePoly) {  // packed polygon slot pc/2, half pc%2
+                            src = reinterpret_cast<const double2*>(a.cpoly + (int64_t)h4.y * MAXV + (pc >> 1)) + (pc & 1);
+                        } else {  // level-pair record piece: field, vertex slot, 16-B piece
+                            const bool f1 = pc >= kTilePoly + kTileRec;
+                            const int pp = pc - (f1 ? kTilePoly + kTileRec : kTilePoly);
+                            const int v = pp / (kPairRec / 2), q = pp - (kPairRec / 2) * v;
+                            const int h = f1 ? h4.w : h4.z;
+                            const int vid = hdi[gg * kTileHdr + 4 + v];
+#if MOPS_PR_LEVEL_MAJOR
+                            const uint32_t ri = (v < h4.x && h >= 1 && h <= a.L - 1)
+                                                    ? (uint32_t)(h - 1) * (uint32_t)a.V + (uint32_t)vid : zrec;
+#else
+                            const uint32_t ri = (v < h4.x && h >= 1 && h <= a.L - 1)
+                                                    ? (uint32_t)vid * (uint32_t)(a.L - 1) + (uint32_t)(h - 1) : zrec;
+#endif
+                            src = reinterpret_cast<const double2*>((f1 ? a.f1.pr : a.f0.pr) + (uint64_t)ri * kPairRec) + q;
+                        }
+                        s_tile[i] = *src;
+                    }
+                }
+                __builtin_amdgcn_wave_barrier();
+                tile = s_tile + g * kTilePieces;
+            }
+        }
         double hx = 0, hy = 0, hz = 0, wv = 0;
         double nx, ny, nz;
         const double alpha = PATH ? (double)step / (double)a.n_steps : 0.0;
         if (EULER) {
-            bool ok = dev::eval_at<MAXV, PATH, PairGroup<PATH, EULER>::value>(hex, c, a.L, a.V, a.f0, a.f1, x, y, z, d, alpha, hint0, hint1, hx, hy, hz, wv);
+            bool ok = dev::eval_at<MAXV, PATH, PairGroup<PATH, EULER>::value>(hex, c, a.L, a.V, a.f0, a.f1, x, y, z, d, alpha, hint0, hint1, hx, hy, hz, wv,
+                                                                              coop, tile);
             if (!ok) { died = (int)step; break; }
             MOPS_MARK(120);
             const double ax = y * hz - z * hy, ay = z * hx - x * hz, az = x * hy - y * hx;
