@@ -586,10 +586,11 @@ def print_prof_counters():
     if os.environ.get("MOPS_PROF_SECTIONS") == "1":
         import ctypes
         from mops_amd import _lib
-        buf = (ctypes.c_uint64 * 8)()
+        buf = (ctypes.c_uint64 * 16)()
         _lib.load().mops_debug_prof(buf)
-        print("prof counters lane-steps, lane walks, lane loads, wave-steps, wave-steps walking, wave-steps loading:",
-              list(buf), file=sys.stderr)
+        print("prof counters lane-steps, lane walks, lane loads, wave-steps, wave-steps walking, wave-steps loading, "
+              "coop wave-steps, coop groups, cells per wave-step (sum), (cell, hint) groups (sum), wave-steps with "
+              "<= 2 cells, with <= 2 groups, wave-steps:", list(buf), file=sys.stderr)
 
 
 def main_chain(args, mesh, dev, world, rank):

@@ -98,6 +98,9 @@ inline int rec_ints_for(int maxv) { return ((1 + 2 * maxv) + 3) / 4 * 4; }
 // front layer, hinted back layer) loads each group's polygon and records ONCE -- one 16-B piece
 // per lane, the pieces of all groups spread over the wave -- into an LDS tile, and its lanes
 // read them from there (ds_read_b128).  Same doubles, same order: bit-identical results.
+#ifndef MOPS_FUSED_RECORDS
+#define MOPS_FUSED_RECORDS 1  // derivation: vertex values computed inside the record build (field_derive)
+#endif
 #ifndef MOPS_COOP_PE
 #define MOPS_COOP_PE 1
 #endif
@@ -105,15 +108,18 @@ inline int rec_ints_for(int maxv) { return ((1 + 2 * maxv) + 3) / 4 * 4; }
 #define MOPS_GR_COOP 1  // level-pair records per LDS round trip in the tile instantiations
 #endif
 #ifndef MOPS_COOP_R
-#define MOPS_COOP_R 4  // tile pieces per live lane at most (fewer live lanes: the lanes gather themselves)
+#define MOPS_COOP_R 12  // tile pieces per live lane at most (fewer live lanes: the lanes gather themselves)
 #endif
 #ifndef MOPS_COOP_G
-#define MOPS_COOP_G 2  // groups per wave with a tile (LDS: 1344 B + a 48-B header each)
+#define MOPS_COOP_G 7  // groups per wave with a tile (LDS: 1520 B + an 80-B header each)
 #endif
 constexpr int kTilePoly = 2 * 7;           // 16-B pieces: 7 packed polygon slots {x, y, z, B_j}
+constexpr int kCellNrm = 22;               // doubles per cell of mops_mesh::d_cnrm: 7 edge normals + pad
+constexpr int kTileNrm = kCellNrm / 2;     // ... as 11 pieces
 constexpr int kTileRec = (kPairRec / 2) * 7;  // 7 level-pair records of one field
-constexpr int kTilePieces = kTilePoly + 2 * kTileRec;  // 84 pieces = 1344 B per group
-constexpr int kTileHdr = 12;               // ints per group header: nv, cell, h0, h1, vid[7], pad
+constexpr int kTileOffNrm = kTilePoly, kTileOffRec = kTilePoly + kTileNrm;
+constexpr int kTilePieces = kTilePoly + kTileNrm + 2 * kTileRec;  // 95 pieces = 1520 B per group
+constexpr int kTileHdr = 20;               // ints per group header: cell, nv, pad x2, front / back record index x 8
 
 }  // namespace
 
@@ -141,6 +147,7 @@ struct mops_mesh {
     // [C][maxv] each cell's polygon in rotated slot order with its Wachspress weights' numerators:
     // slot j = {poly[j-1] (poly[-1] = poly[nv-1]), B_j = area(poly[j-1], poly[j], poly[j+1])}, zeros past nv
     double4* d_cpoly = nullptr;
+    double* d_cnrm = nullptr;    // [C][kCellNrm] IsInMesh edge normals of the rotated polygon slots (maxv 7 meshes)
     double* d_rloc2 = nullptr;       // [C] squared hinted-locate radius (locate_radius_kernel)
     double* d_ring = nullptr;        // [C] hinted-locate ring distance (locate_radius_kernel)
     // grow-only scratch for mops_order_particles (not re-entrant, like the reference's global app)
@@ -180,6 +187,10 @@ struct mops_field {
     // only by fields built from device arrays so mops_field_rebuild_device never allocates
     double* d_ztc = nullptr;
     double* d_velc = nullptr;
+    // d_vel / d_w hold every value (fields uploaded as vertex arrays); false after the fused
+    // derivation (pair_record_fused_kernel), which writes only the records, d_zt and w at level L:
+    // mops_field_export then rebuilds d_vel / d_w from the records (records_to_vertex_kernel)
+    bool vtx_full = true;
     int64_t bytes = 0;
 };
 
@@ -677,7 +688,10 @@ __device__ __forceinline__ bool weights(const Cell<MAXV>& c, int L, int V, doubl
             const double by = wrap ? Y[0] : Y[(i + 1) % MAXV];
             const double bz = wrap ? Z[0] : Z[(i + 1) % MAXV];
             double nx, ny, nz;  // the edge normal X_i x X_{i+1}: cached per cell (load_cell) or computed
-            if (c.lds_n && i < kNrmSlots(MAXV)) {
+            if constexpr (COOP) {  // the tile's copy of the cell's normals (mops_mesh::d_cnrm)
+                const double* tn = reinterpret_cast<const double*>(tpoly + kTilePoly / 2);
+                nx = tn[3 * i]; ny = tn[3 * i + 1]; nz = tn[3 * i + 2];
+            } else if (c.lds_n && i < kNrmSlots(MAXV)) {
                 nx = c.nrm[(3 * i + 0) * kTrajBlock]; ny = c.nrm[(3 * i + 1) * kTrajBlock]; nz = c.nrm[(3 * i + 2) * kTrajBlock];
             } else {
                 nx = Y[i] * bz - Z[i] * by;
@@ -957,8 +971,9 @@ __device__ __forceinline__ int bracket_mono(const Cell<MAXV>& c, const double* w
 #if defined(MOPS_PROF)
 // Event counters for perf experiments (tools/build_variant.sh -DMOPS_PROF), read back with
 // mops_debug_prof: [0] lane-steps, [1] lane walks, [2] lane cell loads, [3] wave-steps,
+// [6] cooperative wave-steps (pathline Euler tile), [7] their groups,
 // [4] wave-steps with a walk, [5] wave-steps with a cell load.  Never set in a product build.
-__device__ unsigned long long g_prof[8];
+__device__ unsigned long long g_prof[16];
 #endif
 
 template <int MAXV, bool PAIR>
@@ -1264,9 +1279,9 @@ __device__ __forceinline__ bool eval_path(const Cell<MAXV>& c, int L, int V, con
     const bool wfin = weights_finite<MAXV, NV>(c, w);
     Pair F, B;
     const int lf = layer_eval<MAXV, true, GR, MOPS_HEX_PAIRS_P ? NV : 0, COOP>(c, w, fast_ok<MAXV, NV>(c, c.mono0, wfin, w), ff, L, d, hint0, F,
-                                                                               tile + kTilePoly);
+                                                                               tile + kTileOffRec);
     const int lb = layer_eval<MAXV, true, GR, MOPS_HEX_PAIRS_P ? NV : 0, COOP>(c, w, fast_ok<MAXV, NV>(c, c.mono1, wfin, w), fb, L, d, hint1, B,
-                                                                               tile + kTilePoly + kTileRec);
+                                                                               tile + kTileOffRec + kTileRec);
     if (lf < 0 || lb < 0) return false;
     const double xf = dmax(F.zk, dmin(d, F.zm));
     const double denf = F.zm - F.zk;
@@ -1330,6 +1345,7 @@ struct TrajArgs {
     const int* __restrict__ order;  // slot -> particle (NULL = identity)
     const int* __restrict__ n_live;  // device count of leading live slots (compaction), NULL = all n
     const double4* __restrict__ cpoly;  // per-cell rotated polygon + Wachspress B_i (mops_mesh::d_cpoly)
+    const double* __restrict__ cnrm;    // per-cell edge normals (mops_mesh::d_cnrm; NULL past maxEdges 7)
     double* px; double* py; double* pz;
     float* depth;
     int* cell;
@@ -1457,18 +1473,20 @@ __global__ void __launch_bounds__(kTrajBlock, (TrajWaves<MAXV, PATH, EULER>::val
     c.id = -1;
     c.nv = 0;
     c.V = a.V;
-    constexpr bool kRC = RCache<MAXV, PATH, EULER>::value, kNrm = LdsNormals<MAXV, PATH, EULER>::value;
+    // cooperative waves (see kTilePieces): the wave's LDS tile and its group headers; their kernel keeps no
+    // per-lane normals (a tiled wave reads its cells' normals from the tile, any other wave computes them)
+    constexpr bool kCoop = PATH && EULER && MAXV == 7 && !RCache<MAXV, PATH, EULER>::value && MOPS_CPOLY &&
+                           MOPS_COOP_PE;
+    constexpr bool kRC = RCache<MAXV, PATH, EULER>::value, kNrm = LdsNormals<MAXV, PATH, EULER>::value && !kCoop;
     __shared__ double s_nrm[kNrm ? 3 * kNrmSlots(MAXV) * kTrajBlock : 1];  // per-lane edge normals (Cell::nrm)
     c.nrm = s_nrm + threadIdx.x;
-    constexpr bool kPairT = kNrm && (PATH ? MOPS_PAIR_TEST_P : MOPS_PAIR_TEST);  // (load_cell resets it with the normals)
+    constexpr bool kPairT = (kNrm || kCoop) && (PATH ? MOPS_PAIR_TEST_P : MOPS_PAIR_TEST);  // (load_cell resets it)
     __shared__ double s_pr2[kPairT ? (MOPS_LDS_COMPACT ? 4 : 5) * kTrajBlock : 1];  // per-lane pair test (Cell::pr2, dev::walk)
     __shared__ float s_rb2[kPairT && MOPS_LDS_COMPACT ? kTrajBlock : 1];
     c.pr2 = s_pr2 + threadIdx.x;
     c.rb2 = s_rb2 + (kPairT && MOPS_LDS_COMPACT ? threadIdx.x : 0);
-    // cooperative waves (see kTilePieces): the wave's LDS tile and its group headers
-    constexpr bool kCoop = PATH && EULER && MAXV == 7 && !kRC && MOPS_CPOLY && MOPS_COOP_PE;
     __shared__ double2 s_tile[kCoop ? MOPS_COOP_G * kTilePieces : 1];
-    __shared__ int4 s_hdr[kCoop ? MOPS_COOP_G * (kTileHdr / 4) : 1];
+    __shared__ uint4 s_hdr[kCoop ? MOPS_COOP_G * (kTileHdr / 4) : 1];
     const int C = a.C;
     // next recording step (the smallest j >= step_begin with (j+1) % rec_period == 0) and its
     // record index, advanced by counting instead of a 64-bit modulo per step
@@ -1478,6 +1496,8 @@ __global__ void __launch_bounds__(kTrajBlock, (TrajWaves<MAXV, PATH, EULER>::val
         rec_k = a.step_begin / a.rec_period;
         rec_next = (rec_k + 1) * a.rec_period - 1;
     }
+    int tcell = -1, tkey = 0;               // cooperative tile: this lane's (cell, hints) at the last fill + group
+    bool have_tile = false, coop_prev = false;  // (wave-uniform)
     for (int64_t step = a.step_begin; step < a.step_end; ++step) {
         MOPS_MARK(100);
         if (step == 0) {  // first_loop (:892-901)
@@ -1557,72 +1577,124 @@ __global__ void __launch_bounds__(kTrajBlock, (TrajWaves<MAXV, PATH, EULER>::val
         bool coop = false;  // wave-uniform: this step's polygon and hinted-layer records come from s_tile
         const double2* tile = nullptr;
         if constexpr (kCoop) {
-            // groups of live lanes with equal (cell, hint0, hint1), found leader by leader with
-            // scalar readlanes + ballots; more than MOPS_COOP_G groups: the lanes gather themselves
-            const uint64_t act = __ballot(1);
-            uint64_t rem = act;
-            int g = 0, G = 0;
-            bool lead = false;
-            while (rem != 0ull && G < MOPS_COOP_G) {
-                const int ld = __builtin_ctzll(rem);
-                const int kc = __builtin_amdgcn_readlane(cell, ld);
-                const int k0 = __builtin_amdgcn_readlane(hint0, ld);
-                const int k1 = __builtin_amdgcn_readlane(hint1, ld);
-                const bool mine = (cell == kc) & (hint0 == k0) & (hint1 == k1);
-                const uint64_t m = __ballot(mine);
-                if (mine) g = G;
-                lead |= ((int)__lane_id() == ld);
-                rem &= ~m;
-                ++G;
-            }
-            // the pieces are spread over the live lanes only (a dead or finished lane has left the
-            // loop): at most MOPS_COOP_R per lane
-            const int nact = __popcll(act);
-            coop = rem == 0ull && G * kTilePieces <= MOPS_COOP_R * nact;
-            if (coop) {
-                if (lead) {  // the group's header: {nv, cell, h0, h1}, vid[0..3], vid[4..6]
-                    int4* hd = s_hdr + g * (kTileHdr / 4);
-                    hd[0] = make_int4(c.nv, cell, hint0, hint1);
-                    hd[1] = make_int4(c.vid[0], c.vid[1], c.vid[2], c.vid[3]);
-                    hd[2] = make_int4(c.vid[4], c.vid[5], c.vid[6], 0);
+            // The tile persists across steps: within a launch the fields are fixed, so a group's pieces
+            // stay valid while no live lane changes its (cell, hint0, hint1) -- cells change ~once per
+            // particle-day at config 3.  Any change regroups the wave and refills the whole tile.
+            const int hk = ((hint0 + 1) << 16) | ((hint1 + 1) << 8);  // (hints >= -1, < 2^7)
+            const bool moved = (cell != tcell) | (hk != (tkey & ~0xff));
+            if (__ballot(moved) != 0ull || !have_tile) {
+                // groups of live lanes with equal (cell, hint0, hint1), found leader by leader with
+                // scalar readlanes + ballots; more than MOPS_COOP_G groups: the lanes gather themselves
+                const uint64_t act = __ballot(1);
+                uint64_t rem = act;
+                int g = 0, G = 0;
+                bool lead = false;
+                while (rem != 0ull && G < MOPS_COOP_G) {
+                    const int ld = __builtin_ctzll(rem);
+                    const int kc = __builtin_amdgcn_readlane(cell, ld);
+                    const int k0 = __builtin_amdgcn_readlane(hint0, ld);
+                    const int k1 = __builtin_amdgcn_readlane(hint1, ld);
+                    const bool mine = (cell == kc) & (hint0 == k0) & (hint1 == k1);
+                    const uint64_t m = __ballot(mine);
+                    if (mine) g = G;
+                    lead |= ((int)__lane_id() == ld);
+                    rem &= ~m;
+                    ++G;
                 }
-                __builtin_amdgcn_wave_barrier();  // (one wave per block: its LDS operations run in order)
-                const int np = G * kTilePieces;
-                const uint32_t zrec = (uint32_t)a.V * (uint32_t)(a.L - 1);
-                const int* hdi = reinterpret_cast<const int*>(s_hdr);
-                // this lane's rank among the live lanes
-                const int rank = (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(act >> 32),
-                                                                __builtin_amdgcn_mbcnt_lo((uint32_t)act, 0u));
-#pragma unroll
-                for (int rr = 0; rr < MOPS_COOP_R; ++rr) {
-                    const int i = rank + nact * rr;
-                    if (i < np) {
-                        const int gg = i / kTilePieces, pc = i - gg * kTilePieces;
-                        const int4 h4 = s_hdr[gg * (kTileHdr / 4)];
-                        const double2* src;
-                        if (pc < kTilePoly) {  // packed polygon slot pc/2, half pc%2
-                            src = reinterpret_cast<const double2*>(a.cpoly + (int64_t)h4.y * MAXV + (pc >> 1)) + (pc & 1);
-                        } else {  // level-pair record piece: field, vertex slot, 16-B piece
-                            const bool f1 = pc >= kTilePoly + kTileRec;
-                            const int pp = pc - (f1 ? kTilePoly + kTileRec : kTilePoly);
-                            const int v = pp / (kPairRec / 2), q = pp - (kPairRec / 2) * v;
-                            const int h = f1 ? h4.w : h4.z;
-                            const int vid = hdi[gg * kTileHdr + 4 + v];
-#if MOPS_PR_LEVEL_MAJOR
-                            const uint32_t ri = (v < h4.x && h >= 1 && h <= a.L - 1)
-                                                    ? (uint32_t)(h - 1) * (uint32_t)a.V + (uint32_t)vid : zrec;
-#else
-                            const uint32_t ri = (v < h4.x && h >= 1 && h <= a.L - 1)
-                                                    ? (uint32_t)vid * (uint32_t)(a.L - 1) + (uint32_t)(h - 1) : zrec;
-#endif
-                            src = reinterpret_cast<const double2*>((f1 ? a.f1.pr : a.f0.pr) + (uint64_t)ri * kPairRec) + q;
-                        }
-                        s_tile[i] = *src;
+                // the pieces are spread over the live lanes only (a dead or finished lane has left the
+                // loop): at most MOPS_COOP_R per lane
+                const int nact = __popcll(act);
+                coop = rem == 0ull && G * kTilePieces <= MOPS_COOP_R * nact;
+    #if defined(MOPS_PROF)
+                // [6] cooperative wave-steps, [7] groups of the waves that were grouped in full (rem == 0);
+                // [8] / [9] distinct cells / distinct (cell, hint0, hint1) per wave-step (unbounded),
+                // [10] / [11] wave-steps with at most 2 of them, [12] wave-steps
+                {
+                    int gc = 0, gf = 0;
+                    for (uint64_t r2 = act; r2 != 0ull; ++gc) {
+                        const int l2 = __builtin_ctzll(r2);
+                        r2 &= ~__ballot(cell == __builtin_amdgcn_readlane(cell, l2));
+                    }
+                    for (uint64_t r2 = act; r2 != 0ull; ++gf) {
+                        const int l2 = __builtin_ctzll(r2);
+                        r2 &= ~__ballot((cell == __builtin_amdgcn_readlane(cell, l2)) &
+                                        (hint0 == __builtin_amdgcn_readlane(hint0, l2)) &
+                                        (hint1 == __builtin_amdgcn_readlane(hint1, l2)));
+                    }
+                    if ((int)__lane_id() == __builtin_ctzll(act)) {
+                        atomicAdd(&dev::g_prof[7], 1ull);  // regroupings
+                        atomicAdd(&dev::g_prof[8], (unsigned long long)gc);
+                        atomicAdd(&dev::g_prof[9], (unsigned long long)gf);
+                        if (gc <= 2) atomicAdd(&dev::g_prof[10], 1ull);
+                        if (gf <= 2) atomicAdd(&dev::g_prof[11], 1ull);
+                        atomicAdd(&dev::g_prof[12], 1ull);
                     }
                 }
-                __builtin_amdgcn_wave_barrier();
-                tile = s_tile + g * kTilePieces;
+    #endif
+                if (coop) {
+                    if (lead) {  // the group's header: {cell, nv}, then each slot's level-pair record index per field
+                        const uint32_t zr = (uint32_t)a.V * (uint32_t)(a.L - 1);
+                        uint32_t r0[8], r1[8];
+    #pragma unroll
+                        for (int v = 0; v < 8; ++v) {
+                            const bool on = v < c.nv && v < MAXV;
+                            const uint32_t vid = (uint32_t)c.vid[v < MAXV ? v : 0];
+    #if MOPS_PR_LEVEL_MAJOR
+                            r0[v] = (on && hint0 >= 1 && hint0 <= a.L - 1) ? (uint32_t)(hint0 - 1) * (uint32_t)a.V + vid : zr;
+                            r1[v] = (on && hint1 >= 1 && hint1 <= a.L - 1) ? (uint32_t)(hint1 - 1) * (uint32_t)a.V + vid : zr;
+    #else
+                            r0[v] = (on && hint0 >= 1 && hint0 <= a.L - 1) ? vid * (uint32_t)(a.L - 1) + (uint32_t)(hint0 - 1) : zr;
+                            r1[v] = (on && hint1 >= 1 && hint1 <= a.L - 1) ? vid * (uint32_t)(a.L - 1) + (uint32_t)(hint1 - 1) : zr;
+    #endif
+                        }
+                        uint4* hd = reinterpret_cast<uint4*>(s_hdr + g * (kTileHdr / 4));
+                        hd[0] = make_uint4((uint32_t)cell, (uint32_t)c.nv, 0u, 0u);
+                        hd[1] = make_uint4(r0[0], r0[1], r0[2], r0[3]);
+                        hd[2] = make_uint4(r0[4], r0[5], r0[6], r0[7]);
+                        hd[3] = make_uint4(r1[0], r1[1], r1[2], r1[3]);
+                        hd[4] = make_uint4(r1[4], r1[5], r1[6], r1[7]);
+                    }
+                    __builtin_amdgcn_wave_barrier();  // (one wave per block: its LDS operations run in order)
+                    const int np = G * kTilePieces;
+                    const uint32_t* hdi = reinterpret_cast<const uint32_t*>(s_hdr);
+                    const double2* cpoly2 = reinterpret_cast<const double2*>(a.cpoly);
+                    const double2* cnrm2 = reinterpret_cast<const double2*>(a.cnrm);
+                    const double2* pr0 = reinterpret_cast<const double2*>(a.f0.pr);
+                    const double2* pr1 = reinterpret_cast<const double2*>(a.f1.pr);
+                    // this lane's rank among the live lanes
+                    const int rank = (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(act >> 32),
+                                                                    __builtin_amdgcn_mbcnt_lo((uint32_t)act, 0u));
+    #pragma unroll
+                    for (int rr = 0; rr < MOPS_COOP_R; ++rr) {
+                        const int i = rank + nact * rr;
+                        if (i < np) {  // piece pc of group gg: polygon, normals, front records, back records
+                            const int gg = i / kTilePieces, pc = i - gg * kTilePieces;
+                            const uint32_t cl = hdi[gg * kTileHdr];
+                            const bool isp = pc < kTileOffNrm, isn = pc < kTileOffRec;
+                            const bool f1 = pc >= kTileOffRec + kTileRec;
+                            const int pp = isn ? 0 : pc - (f1 ? kTileOffRec + kTileRec : kTileOffRec);
+                            const int v = pp / (kPairRec / 2), q = pp - (kPairRec / 2) * v;
+                            const uint32_t ri = hdi[gg * kTileHdr + 4 + (f1 ? 8 : 0) + v];
+                            const double2* base = isp ? cpoly2 : (isn ? cnrm2 : (f1 ? pr1 : pr0));
+                            const uint64_t idx = isp ? ((uint64_t)cl * MAXV + (uint32_t)(pc >> 1)) * 2 + (uint32_t)(pc & 1)
+                                                     : (isn ? (uint64_t)cl * kTileNrm + (uint32_t)(pc - kTileOffNrm)
+                                                            : (uint64_t)ri * (kPairRec / 2) + (uint32_t)q);
+                            s_tile[i] = base[idx];
+                        }
+                    }
+                    __builtin_amdgcn_wave_barrier();
+                }
+                tcell = cell;
+                tkey = hk | (coop ? g : 0xff);
+                have_tile = true;
+                coop_prev = coop;
+            } else {
+                coop = coop_prev;
             }
+            if (coop) tile = s_tile + (tkey & 0xff) * kTilePieces;
+#if defined(MOPS_PROF)
+            if ((int)__lane_id() == __builtin_ctzll(__ballot(1)) && coop) atomicAdd(&dev::g_prof[6], 1ull);
+#endif
         }
         double hx = 0, hy = 0, hz = 0, wv = 0;
         double nx, ny, nz;
@@ -2450,8 +2522,12 @@ __global__ void mono_kernel(int64_t C, int maxv, int rec_ints, const int* cellre
 // poly[j], poly[j+1]) -- the same device arithmetic as the in-kernel computation, so
 // bit-identical -- as one 32-B {x, y, z, B_j} per slot: the modes that re-read the polygon per
 // evaluation (pathline) load a slot with 2 VMEM instructions instead of a vertex double4 + B_j.
+// ... and (cnrm != NULL, MAXV 7) the IsInMesh edge normals n_i = X_i x X_{i+1} of the rotated slots,
+// the products load_cell and dev::weights form (same operands, same order), [C][kCellNrm]: the
+// cooperative waves' tile takes them from here
 template <int MAXV>
-__global__ void cell_poly_kernel(int64_t C, const int* cellrec, const double4* vxyz, double4* cpoly) {
+__global__ void cell_poly_kernel(int64_t C, const int* cellrec, const double4* vxyz, double4* cpoly,
+                                 double* cnrm = nullptr) {
     const int64_t c = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (c >= C) return;
     constexpr int REC = ((1 + 2 * MAXV) + 3) / 4 * 4;
@@ -2481,7 +2557,18 @@ __global__ void cell_poly_kernel(int64_t C, const int* cellrec, const double4* v
             o = make_double4(qx, qy, qz, dev::tri_area(qx, qy, qz, x[i], y[i], z[i], nx, ny, nz));
         }
         cpoly[c * MAXV + i] = o;
+        if (cnrm && 3 * i + 2 < kCellNrm) {
+            double* n = cnrm + c * kCellNrm + 3 * i;
+            if (i < nv) {  // X_i = (qx, qy, qz), X_{i+1} = poly[i] = (x[i], y[i], z[i])
+                n[0] = o.y * z[i] - o.z * y[i];
+                n[1] = o.z * x[i] - o.x * z[i];
+                n[2] = o.x * y[i] - o.y * x[i];
+            } else {
+                n[0] = 0.0; n[1] = 0.0; n[2] = 0.0;
+            }
+        }
     }
+    if (cnrm) cnrm[c * kCellNrm + kCellNrm - 1] = 0.0;
 }
 
 // Level-pair records (mops_field::d_pr), one 16-B chunk per thread so that a wave's
@@ -2566,6 +2653,87 @@ __global__ void __launch_bounds__(256) pair_record_tiled_kernel(int64_t V, int L
         const int64_t rec = (int64_t)(k0 + kl) * V + v0 + vl;
         reinterpret_cast<double2*>(pr)[rec * (kPairRec / 2) + q] = val;
     }
+}
+
+// The same level-major records straight from the CELL arrays: each tile's vertex values are the
+// barycentric combinations cell_to_vertex_bary_kernel computes (b.x*a0 + b.y*a1 + b.z*a2 of the
+// three cellsOnVertex, 0 at a boundary vertex; same operands, same order: the same doubles), so the
+// vertex velocity and vertical-velocity arrays are never written and read back (36 GB of traffic
+// per oRRS18to6 snapshot).  Also writes the vertex zTop (the bracket's column) and w at level L,
+// the one value no record holds.
+template <bool HAS_W>
+__global__ void __launch_bounds__(256) pair_record_fused_kernel(int64_t V, int L, const int* __restrict__ cov,
+                                                                const double4* __restrict__ bary,
+                                                                const double* __restrict__ ztc,
+                                                                const double* __restrict__ velc,
+                                                                const double* __restrict__ wc,
+                                                                double* __restrict__ zt, double* __restrict__ w_out,
+                                                                double* __restrict__ pr) {
+    __shared__ double sz[kRecTV][kRecTK + 1], sw[kRecTV][kRecTK + 1], su[kRecTV][kRecTK + 1][3];
+    const int64_t v0 = (int64_t)blockIdx.x * kRecTV;
+    const int k0 = (int)blockIdx.y * kRecTK;
+    const int nk = min(kRecTK, L - 1 - k0);
+    const int nv = (int)min<int64_t>(kRecTV, V - v0);
+    const int t = (int)threadIdx.x;
+    const bool last = k0 + nk == L - 1;  // this tile row holds level L-1
+    for (int i = t; i < kRecTV * (kRecTK + 1); i += blockDim.x) {
+        const int vl = i / (kRecTK + 1), kl = i - vl * (kRecTK + 1);
+        if (vl < nv && kl <= nk) {
+            const int64_t v = v0 + vl;
+            const int k = k0 + kl;
+            const double4 b = bary[v];
+            double z = 0.0, w = 0.0, u0 = 0.0, u1 = 0.0, u2 = 0.0, wl = 0.0;
+            if (b.w != 0.0) {
+                const int64_t c0 = cov[3 * v], c1 = cov[3 * v + 1], c2 = cov[3 * v + 2];
+                z = b.x * ztc[c0 * L + k] + b.y * ztc[c1 * L + k] + b.z * ztc[c2 * L + k];
+                const double* a0 = velc + (c0 * L + k) * 3;
+                const double* a1 = velc + (c1 * L + k) * 3;
+                const double* a2 = velc + (c2 * L + k) * 3;
+                u0 = b.x * a0[0] + b.y * a1[0] + b.z * a2[0];
+                u1 = b.x * a0[1] + b.y * a1[1] + b.z * a2[1];
+                u2 = b.x * a0[2] + b.y * a1[2] + b.z * a2[2];
+                if constexpr (HAS_W) {
+                    w = b.x * wc[c0 * (L + 1) + k] + b.y * wc[c1 * (L + 1) + k] + b.z * wc[c2 * (L + 1) + k];
+                    if (last && kl == nk)
+                        wl = b.x * wc[c0 * (L + 1) + L] + b.y * wc[c1 * (L + 1) + L] + b.z * wc[c2 * (L + 1) + L];
+                }
+            }
+            sz[vl][kl] = z; sw[vl][kl] = w;
+            su[vl][kl][0] = u0; su[vl][kl][1] = u1; su[vl][kl][2] = u2;
+            if (kl < nk || last) zt[v * L + k] = z;  // (levels shared by two tile rows written once)
+            if (last && kl == nk) w_out[v * (L + 1) + L] = wl;
+        }
+    }
+    __syncthreads();
+    for (int i = t; i < nk * kRecTV * (kPairRec / 2); i += blockDim.x) {
+        const int rl = i / (kPairRec / 2), q = i - rl * (kPairRec / 2);
+        const int kl = rl / kRecTV, vl = rl - kl * kRecTV;
+        if (vl >= nv) continue;
+        double2 val;
+        if (q == 0) val = make_double2(sz[vl][kl], sz[vl][kl + 1]);
+        else if (q == 1) val = make_double2(sw[vl][kl], sw[vl][kl + 1]);
+        else if (q == 2) val = make_double2(su[vl][kl][0], su[vl][kl][1]);
+        else if (q == 3) val = make_double2(su[vl][kl][2], su[vl][kl + 1][0]);
+        else val = make_double2(su[vl][kl + 1][1], su[vl][kl + 1][2]);
+        const int64_t rec = (int64_t)(k0 + kl) * V + v0 + vl;
+        reinterpret_cast<double2*>(pr)[rec * (kPairRec / 2) + q] = val;
+    }
+}
+
+// mops_field_export of a fused field: the vertex velocity [V][L][3] and vertical velocity levels
+// 0..L-1 back out of the level-major records (level j from record j, level L-1 from record L-2)
+__global__ void records_to_vertex_kernel(int64_t V, int L, const double* __restrict__ pr, double* __restrict__ vel,
+                                         double* __restrict__ w) {
+    const int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (idx >= V * L) return;
+    const int64_t v = idx / L;
+    const int j = (int)(idx - v * L);
+    const bool hi = j == L - 1;  // the second half of record L-2
+    const double* r = pr + ((int64_t)(hi ? j - 1 : j) * V + v) * kPairRec;
+    w[v * (L + 1) + j] = hi ? r[3] : r[2];
+    vel[idx * 3 + 0] = hi ? r[7] : r[4];
+    vel[idx * 3 + 1] = hi ? r[8] : r[5];
+    vel[idx * 3 + 2] = hi ? r[9] : r[6];
 }
 
 __device__ __forceinline__ uint64_t spread3(uint64_t v) {  // 21 bits -> every third bit
@@ -2706,7 +2874,7 @@ void free_mesh(mops_mesh* m) {
     if (!m) return;
     (void)hipFree(m->d_cellrec); (void)hipFree(m->d_cxyz); (void)hipFree(m->d_vxyz); (void)hipFree(m->d_cov);
     (void)hipFree(m->d_bary);
-    (void)hipFree(m->d_bkeys); (void)hipFree(m->d_bcells); (void)hipFree(m->d_hkeys); (void)hipFree(m->d_hval); (void)hipFree(m->d_cell_rank); (void)hipFree(m->d_cpoly); (void)hipFree(m->d_rloc2); (void)hipFree(m->d_ring);
+    (void)hipFree(m->d_bkeys); (void)hipFree(m->d_bcells); (void)hipFree(m->d_hkeys); (void)hipFree(m->d_hval); (void)hipFree(m->d_cell_rank); (void)hipFree(m->d_cpoly); (void)hipFree(m->d_cnrm); (void)hipFree(m->d_rloc2); (void)hipFree(m->d_ring);
     (void)hipFree(m->d_scratch);
     (void)hipFree(m->d_eoc); (void)hipFree(m->d_coe); (void)hipFree(m->d_exyz); (void)hipFree(m->d_rbf_coef);
     (void)hipFree(m->d_rbf_slot);
@@ -2788,11 +2956,11 @@ const char* mops_last_error(void) { return g_last_error.c_str(); }
 #if defined(MOPS_PROF)
 // experiment builds only: read and clear the event counters (dev::g_prof)
 int mops_debug_prof(uint64_t* out) {
-    unsigned long long h[8];
+    unsigned long long h[16];
     if (hipDeviceSynchronize() != hipSuccess) return -1;
     if (hipMemcpyFromSymbol(h, HIP_SYMBOL(dev::g_prof), sizeof(h)) != hipSuccess) return -1;
-    for (int i = 0; i < 8; ++i) out[i] = h[i];
-    const unsigned long long z[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    for (int i = 0; i < 16; ++i) out[i] = h[i];
+    const unsigned long long z[16] = {};
     if (hipMemcpyToSymbol(HIP_SYMBOL(dev::g_prof), z, sizeof(z)) != hipSuccess) return -1;
     return 0;
 }
@@ -2999,8 +3167,9 @@ mops_status mops_mesh_create(const mops_mesh_desc* desc, void* stream, mops_mesh
                                                         m->bucket_h, m->d_cellrec, m->rec_ints, m->maxv,
                                                         m->d_rloc2, m->d_ring);
     if ((st = dmalloc(&m->d_cpoly, (size_t)(C * m->maxv), &acc)) != MOPS_OK) { free_mesh(m); return st; }
+    if (m->maxv == 7 && (st = dmalloc(&m->d_cnrm, (size_t)(C * kCellNrm), &acc)) != MOPS_OK) { free_mesh(m); return st; }
     switch (m->maxv) {
-        case 7: cell_poly_kernel<7><<<grid_for(C), kBlock, 0, s>>>(C, m->d_cellrec, m->d_vxyz, m->d_cpoly); break;
+        case 7: cell_poly_kernel<7><<<grid_for(C), kBlock, 0, s>>>(C, m->d_cellrec, m->d_vxyz, m->d_cpoly, m->d_cnrm); break;
         case 12: cell_poly_kernel<12><<<grid_for(C), kBlock, 0, s>>>(C, m->d_cellrec, m->d_vxyz, m->d_cpoly); break;
         default: cell_poly_kernel<20><<<grid_for(C), kBlock, 0, s>>>(C, m->d_cellrec, m->d_vxyz, m->d_cpoly); break;
     }
@@ -3086,11 +3255,20 @@ mops_status mops_cell_center_velocity_rbf(const mops_mesh* m, const double* d_no
     return MOPS_OK;
 }
 
-static mops_status compute_mono(const mops_mesh* mesh, mops_field* f, hipStream_t s) {
+static mops_status alloc_records(const mops_mesh* mesh, mops_field* f, hipStream_t s) {
     const int64_t npr = mesh->V * (int64_t)std::max(mesh->L - 1, 0);
     // + one all-zero record at index npr: pair_sums reads it for v >= nv
     if (!f->d_pr) MOPS_TRY(dmalloc(&f->d_pr, (size_t)((npr + 1) * kPairRec), &f->bytes));
     HIP_TRY(hipMemsetAsync(f->d_pr + npr * kPairRec, 0, kPairRec * sizeof(double), s));
+    return MOPS_OK;
+}
+
+static mops_status compute_flags(const mops_mesh* mesh, mops_field* f, hipStream_t s);
+
+// records from the vertex arrays (fields uploaded as vertex arrays), then the fast-path flags
+static mops_status compute_mono(const mops_mesh* mesh, mops_field* f, hipStream_t s) {
+    const int64_t npr = mesh->V * (int64_t)std::max(mesh->L - 1, 0);
+    MOPS_TRY(alloc_records(mesh, f, s));
 #if MOPS_PR_LEVEL_MAJOR
     if (npr > 0) {
         const dim3 grid((unsigned)((mesh->V + kRecTV - 1) / kRecTV), (unsigned)((mesh->L - 1 + kRecTK - 1) / kRecTK));
@@ -3108,6 +3286,10 @@ static mops_status compute_mono(const mops_mesh* mesh, mops_field* f, hipStream_
                                                                            f->d_w, f->d_pr);
     }
 #endif
+    return compute_flags(mesh, f, s);
+}
+
+static mops_status compute_flags(const mops_mesh* mesh, mops_field* f, hipStream_t s) {
     if (!f->d_mono) MOPS_TRY(dmalloc(&f->d_mono, (size_t)mesh->C, &f->bytes));
     if (!f->d_vmono) MOPS_TRY(dmalloc(&f->d_vmono, (size_t)mesh->V, &f->bytes));
     if (!f->d_vzero) MOPS_TRY(dmalloc(&f->d_vzero, (size_t)mesh->V, &f->bytes));
@@ -3194,13 +3376,31 @@ static mops_status field_derive(const mops_mesh* mesh, mops_field* f, const mops
     if (!f->d_w) MOPS_TRY(dmalloc(&f->d_w, (size_t)(V * (L + 1)), &f->bytes));
     cell_ztop_tiled_kernel<<<(unsigned)((C + kZtCells - 1) / kZtCells), 256, (size_t)kZtCells * L * sizeof(double), s>>>(
         C, L, d->h_layer_thickness, bot, ssh, ztc);
-    cell_to_vertex_bary_kernel<1><<<grid_for(V * L), kBlock, 0, s>>>(V, L, mesh->d_cov, mesh->d_bary, ztc, f->d_zt, 0);
     if (d->h_zonal_velocity && d->h_meridional_velocity) {  // the live path (MOPSApp.cpp:113)
         center_vel_zm_kernel<<<grid_for(C * L), kBlock, 0, s>>>(C, L, mesh->d_cxyz, d->h_zonal_velocity,
                                                                 d->h_meridional_velocity, velc);
     } else {  // edge normals only: the RBF reconstruction (MPASOSolution::calcCellCenterVelocity)
         MOPS_TRY(mops_cell_center_velocity_rbf(mesh, d->h_normal_velocity, velc, s));
     }
+#if MOPS_PR_LEVEL_MAJOR && MOPS_FUSED_RECORDS
+    if (L >= 2) {
+        // CalcCellVertexZtop / CalcCellVertexVelocity / CalcCellVertexVertVelocity fused into the
+        // level-pair record build (pair_record_fused_kernel)
+        MOPS_TRY(alloc_records(mesh, f, s));
+        const dim3 grid((unsigned)((V + kRecTV - 1) / kRecTV), (unsigned)((L - 1 + kRecTK - 1) / kRecTK));
+        if (d->h_vert_velocity_top)
+            pair_record_fused_kernel<true><<<grid, 256, 0, s>>>(V, L, mesh->d_cov, mesh->d_bary, ztc, velc,
+                                                                d->h_vert_velocity_top, f->d_zt, f->d_w, f->d_pr);
+        else
+            pair_record_fused_kernel<false><<<grid, 256, 0, s>>>(V, L, mesh->d_cov, mesh->d_bary, ztc, velc, nullptr,
+                                                                 f->d_zt, f->d_w, f->d_pr);
+        f->vtx_full = false;
+        MOPS_TRY(compute_flags(mesh, f, s));
+        HIP_TRY(hipGetLastError());
+        return MOPS_OK;
+    }
+#endif
+    cell_to_vertex_bary_kernel<1><<<grid_for(V * L), kBlock, 0, s>>>(V, L, mesh->d_cov, mesh->d_bary, ztc, f->d_zt, 0);
     cell_to_vertex_bary_kernel<3><<<grid_for(V * L), kBlock, 0, s>>>(V, L, mesh->d_cov, mesh->d_bary, velc, f->d_vel, 0);
     if (d->h_vert_velocity_top) {
         cell_to_vertex_bary_kernel<1><<<grid_for(V * (L + 1)), kBlock, 0, s>>>(V, L + 1, mesh->d_cov, mesh->d_bary,
@@ -3285,6 +3485,9 @@ mops_status mops_field_export(const mops_field* f, double* h_zt, double* h_vel, 
     hipStream_t s = (hipStream_t)stream;
     const size_t V = (size_t)f->V, L = (size_t)f->L;
     if (h_zt) HIP_TRY(hipMemcpyAsync(h_zt, f->d_zt, V * L * sizeof(double), hipMemcpyDeviceToHost, s));
+    if ((h_vel || h_w) && !f->vtx_full && L >= 2)  // fused field: rebuild the vertex arrays from the records
+        records_to_vertex_kernel<<<grid_for((int64_t)(V * L)), kBlock, 0, s>>>((int64_t)V, (int)L, f->d_pr, f->d_vel,
+                                                                               f->d_w);
     if (h_vel) HIP_TRY(hipMemcpyAsync(h_vel, f->d_vel, V * L * 3 * sizeof(double), hipMemcpyDeviceToHost, s));
     if (h_w) HIP_TRY(hipMemcpyAsync(h_w, f->d_w, V * (L + 1) * sizeof(double), hipMemcpyDeviceToHost, s));
     HIP_TRY(hipStreamSynchronize(s));
@@ -3483,6 +3686,7 @@ mops_status mops_traj_advance(const mops_mesh* mesh, const mops_field* front, co
     a.order = p->d_order;
     a.n_live = p->d_n_live;
     a.cpoly = mesh->d_cpoly;
+    a.cnrm = mesh->d_cnrm;
     a.px = p->d_x; a.py = p->d_y; a.pz = p->d_z; a.depth = p->d_depth; a.cell = p->d_cell; a.death = p->d_death_step;
     a.n = p->n;
     a.step_begin = step_begin; a.step_end = step_end; a.n_steps = n_steps;

@@ -298,15 +298,19 @@ class ParticleSet:
         self._c = cfg.ctype()
         self.reorder(stream=torch.cuda.current_stream(dev).cuda_stream)
 
-    def reorder(self, stream=None):
+    def reorder(self, stream=None, records_written: int | None = None):
         """Locality order of the particles by their current cell (mops_order_particles), applied by permuting
-        the SoA state (and any records already written) so slot s holds particle ids[s]."""
+        the SoA state (and the records already written: all slots, or the first ``records_written`` --
+        the launches from the current step write every later slot) so slot s holds particle ids[s]."""
         L.check(L.load().mops_order_particles(self.mesh.handle, self.n, C.c_void_p(self.cell.data_ptr()),
                                               C.c_void_p(self.order.data_ptr()), _stream_handle(stream)),
                 "mops_order_particles")
         if not self.use_order or self.n == 0:
             return
-        self._apply_order(self.order, 0, self.n, stream, self.records.shape[0] if self._written else 0)
+        slots = self.records.shape[0] if self._written else 0
+        if records_written is not None:
+            slots = min(slots, max(0, int(records_written)))
+        self._apply_order(self.order, 0, self.n, stream, slots)
 
     _STATE = (("x", 8), ("y", 8), ("z", 8), ("depth", 4), ("cell", 4), ("death", 4), ("ids", 4), ("seeds", 24))
 

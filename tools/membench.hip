@@ -100,6 +100,26 @@ __global__ void __launch_bounds__(256) mb_l1_bcast(const double2* __restrict__ a
     out[(int64_t)blockIdx.x * blockDim.x + threadIdx.x] = s;
 }
 
+// the same L1-resident re-reads with only some lanes of each wave active: mode 0 = 16 lanes spread
+// (every 4th), 1 = 16 contiguous lanes, 2 = 48 lanes, 3 = 1 lane -- does the TD return cost scale
+// with the active lanes of a wave-instruction?
+__global__ void __launch_bounds__(256) mb_l1_partial(const double2* __restrict__ a, int iters, int mode, double* out) {
+    const double2* base = a + (int64_t)blockIdx.x * 256;
+    const int lane = threadIdx.x & 63;
+    const bool on = mode == 0 ? (lane & 3) == 0 : mode == 1 ? lane < 16 : mode == 2 ? lane < 48 : lane == 0;
+    double s = 0.0;
+    if (on) {
+        for (int k = 0; k < iters; k += 4) {
+#pragma unroll
+            for (int u = 0; u < 4; ++u) {
+                const double2 v = base[(threadIdx.x + 64 * u + k) & 255];
+                s += v.x + v.y;
+            }
+        }
+    }
+    out[(int64_t)blockIdx.x * blockDim.x + threadIdx.x] = s;
+}
+
 static float time_ms(hipEvent_t a, hipEvent_t b) {
     float ms = 0.f;
     CK(hipEventElapsedTime(&ms, a, b));
@@ -190,6 +210,18 @@ int main(int argc, char** argv) {
         CK(hipEventSynchronize(e1));
         printf("{\"kernel\": \"mb_l1_bcast\", \"rep\": %d, \"ms\": %.4f, \"lane_bytes\": %lld, \"cus\": %d}\n", r,
                time_ms(e0, e1), (long long)nblk * 256 * iters * 16ll, ncu);
+    }
+    for (int mode = 0; mode < 4; ++mode) {
+        const int active = mode == 0 ? 16 : mode == 1 ? 16 : mode == 2 ? 48 : 1;
+        for (int r = 0; r < reps; ++r) {
+            CK(hipEventRecord(e0));
+            mb_l1_partial<<<nblk, 256>>>(l1, iters, mode, out);
+            CK(hipEventRecord(e1));
+            CK(hipEventSynchronize(e1));
+            printf("{\"kernel\": \"mb_l1_partial\", \"mode\": %d, \"active_lanes\": %d, \"rep\": %d, \"ms\": %.4f, "
+                   "\"lane_bytes\": %lld, \"cus\": %d}\n", mode, active, r, time_ms(e0, e1),
+                   (long long)nblk * 4 * active * iters * 16ll, ncu);
+        }
     }
     CK(hipFree(l1));
     CK(hipFree(out));
