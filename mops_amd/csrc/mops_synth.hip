@@ -53,3 +53,9 @@ extern "C" int mops_synth_snapshot(int64_t C, int L, const double* lat, const do
                                                              u, v, wv);
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }
+
+// the source's identity, stamped by __graft_entry__.build_synth (rebuilt when it differs)
+#ifndef MOPS_SYNTH_BUILD_ID
+#define MOPS_SYNTH_BUILD_ID "unstamped"
+#endif
+extern "C" __attribute__((used)) const char* mops_synth_build_id() { return MOPS_SYNTH_BUILD_ID; }

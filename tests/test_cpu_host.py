@@ -354,3 +354,23 @@ def test_remove_nan_cpp_driver_compiles(engine_lib, tmp_path):
                     os.path.join(ROOT, "tests", "cpp", "remove_nan_api.cpp"), "-L" + libdir, "-lmops_traj",
                     "-Wl,-rpath," + libdir, "-Wl,-rpath-link,/opt/rocm/lib", "-o", exe], check=True)
     assert os.path.exists(exe)
+
+
+def test_synth_library_rebuilds_by_build_id(tmp_path, monkeypatch):
+    """libmops_synth.so (configs 4/5 snapshot generator) carries its source's id and is rebuilt when the
+    stamp differs -- file times play no part (a stale library could otherwise feed configs 4/5)."""
+    import shutil
+    import __graft_entry__ as g
+    from mops_amd import _build_id
+    if shutil.which("hipcc") is None:
+        pytest.skip("no hipcc")
+    g.build_synth()
+    assert _build_id.stamped_id(g.SYNTH_OUT) == g.synth_build_id()
+    stale = tmp_path / "libmops_synth.so"
+    stale.write_bytes(open(g.SYNTH_OUT, "rb").read().replace(g.synth_build_id().encode(), b"0" * 16))
+    monkeypatch.setattr(g, "SYNTH_OUT", str(stale))
+    calls = []
+    real = g.subprocess.run
+    monkeypatch.setattr(g.subprocess, "run", lambda cmd, **k: calls.append(cmd) or real(cmd, **k))
+    g.build_synth()
+    assert calls and _build_id.stamped_id(str(stale)) == g.synth_build_id()
