@@ -161,6 +161,10 @@ def engine_build_id() -> str:
 
 
 PEAK_FP64_TFLOPS = 78.6  # MI355X FP64 vector (spec; half of the guide's 157.3 TF FP32 vector rate)
+# vector-L1 / texture-data return: 64 B per clock per CU (measured: tools/membench.hip mb_l1_x4 moves 64 B per
+# TD-busy cycle at 97% TD busy, 38.0 TB/s chip-wide; one TCP tag access = 64 B), x 256 CUs x 2.4 GHz
+PEAK_L1_RETURN_GBS = 64.0 * 256 * 2.4
+L1_MEASURED_GBS = 38.0e3
 
 
 def measured_entry(key: str):
@@ -218,6 +222,20 @@ def fp64_block(key: str, unit_s: float):
             "flops_per_unit": fl, "source": src + " SQ_INSTS_VALU_{ADD,MUL,FMA}_F64 x 64 lanes (fma = 2)"}
 
 
+def l1_block(key: str, unit_s: float):
+    """The memory-return view that binds the gather kernels: bytes the vector L1 returned to the lanes
+    (TCP_TOTAL_CACHE_ACCESSES x 64 B, rocprofv3) over the unit's time, against the TD return peak."""
+    e, src = measured_entry(key)
+    acc = e.get("tcp_accesses_per_unit") if e else None
+    if acc is None:
+        return {"achieved": None, "peak": PEAK_L1_RETURN_GBS, "unit": "GB/s", "frac": None, "source": src}
+    ach = acc * 64.0 / unit_s / 1e9
+    return {"achieved": ach, "peak": PEAK_L1_RETURN_GBS, "peak_measured": L1_MEASURED_GBS, "unit": "GB/s",
+            "frac": ach / PEAK_L1_RETURN_GBS, "td_busy": e.get("td_busy"),
+            "l1_to_l2_bytes_per_unit": (e.get("l1_to_l2_requests_per_unit") or 0.0) * 128.0,
+            "source": src + " TCP_TOTAL_CACHE_ACCESSES_sum x 64 B, TD_TD_BUSY_sum / 256 over GRBM_GUI_ACTIVE / 8"}
+
+
 def roofline_block(kernel: str, avg_kernel_s: float, psteps_per_launch: float, B: float, traffic_key: str,
                    per: str = "launch") -> dict:
     """The bench line's roofline: HBM GB/s MEASURED by rocprofv3 PMC counters (per launch) over the
@@ -235,9 +253,14 @@ def roofline_block(kernel: str, avg_kernel_s: float, psteps_per_launch: float, B
         "frac": (achieved / PEAK_HBM_GBS) if achieved is not None else None,
         "traffic": traffic,
         "traffic_source": src,
-        "limiter": ("not DRAM: dependent per-lane gathers (L1/TA-served) and FP64 VALU issue at 3 waves/SIMD "
-                    "(DESIGN.md section 3)"),
+        "limiter": ("not DRAM: the texture-data return of the per-lane gathers (l1_return) together with FP64 VALU "
+                    "issue and gather latency at 3 waves/SIMD (DESIGN.md section 3)"),
         "fp64_valu": fp64_block(traffic_key, avg_kernel_s),
+        "l1_return": l1_block(traffic_key, avg_kernel_s),
+        "traffic_correction": ("bytes = 2 x FETCH_SIZE + WRITE_SIZE: the gfx950 factor 1/2 holds for this kernel's "
+                               "scattered 80-B record reads too (tools/membench.hip: 4 GiB streamed -> FETCH_SIZE "
+                               "0.500 of the bytes; 2^25 random 80-B records, one per 128-B line -> 2 x FETCH_SIZE "
+                               "= 1.03 x the lines), DESIGN.md section 3.2"),
         "kernel": kernel,
         "timed_unit": per,
         "particle_steps_per_launch": psteps_per_launch,

@@ -520,7 +520,7 @@ struct Cell {
     // poly[k], p) are the slot pair (k, k+1), wrapping to slot 0 only at k = nv-1
     double x[MAXV], y[MAXV], z[MAXV];
     double B[MAXV];  // Wachspress B_i = area(poly[i-1], poly[i], poly[i+1]) (depends on the polygon only)
-    bool lds_n;         // compile-time constant per kernel (load_cell<MAXV, RC, NRM>): nrm below is live
+    bool lds_n;         // nrm below is live: constant per kernel, or the cooperative kernel's per-wave mode
     // lds_n: IsInMesh edge normals n_i = X_i x X_{i+1} (slot pairs as in dev::weights), computed
     // by load_cell into this lane's LDS column: component j of slot i at nrm[(3 * i + j) * kTrajBlock]
     double* nrm;
@@ -533,11 +533,13 @@ struct Cell {
     const double4* __restrict__ cpoly;  // rc == false: per-cell rotated polygon + B_i [C][MAXV] (cell_poly_kernel)
 };
 
-template <int MAXV, bool RC, bool NRM, bool PT>
+// NRMC (the cooperative kernel): the lane's normals, when it keeps them (c.lds_n, a wave-uniform
+// runtime mode there), are copied from the per-cell array mops_mesh::d_cnrm -- the same products
+template <int MAXV, bool RC, bool NRM, bool PT, bool NRMC = false>
 __device__ __forceinline__ void load_cell(Cell<MAXV>& c, int cell, const int* __restrict__ cellrec,
                                           const double4* __restrict__ vxyz, const uint32_t* __restrict__ mono0,
                                           const uint32_t* __restrict__ mono1, const double4* __restrict__ cxyz,
-                                          const double4* __restrict__ cpoly) {
+                                          const double4* __restrict__ cpoly, const double* __restrict__ cnrm = nullptr) {
     c.mono0 = mono0[cell];
     c.mono1 = mono1[cell];
     {
@@ -560,7 +562,6 @@ __device__ __forceinline__ void load_cell(Cell<MAXV>& c, int cell, const int* __
     c.nv = buf[0];
     const int nv = c.nv;
     c.rc = RC;
-    c.lds_n = NRM;
 #pragma unroll
     for (int k = 0; k < MAXV; ++k) c.vid[k] = buf[1 + k];
     c.vlast = 0;
@@ -571,7 +572,13 @@ __device__ __forceinline__ void load_cell(Cell<MAXV>& c, int cell, const int* __
         c.vxyz = vxyz;
         c.cpoly = cpoly;
     }
-    if constexpr (RC || NRM) {
+    if constexpr (NRMC) {
+        if (c.lds_n) {
+            const double* src = cnrm + (int64_t)cell * kCellNrm;
+#pragma unroll
+            for (int k = 0; k < 3 * kNrmSlots(MAXV); ++k) c.nrm[k * kTrajBlock] = src[k];
+        }
+    } else if constexpr (RC || NRM) {
         double px[MAXV], py[MAXV], pz[MAXV];  // natural order
 #pragma unroll
         for (int k = 0; k < MAXV; ++k) {
@@ -1477,15 +1484,19 @@ __global__ void __launch_bounds__(kTrajBlock, (TrajWaves<MAXV, PATH, EULER>::val
     // per-lane normals (a tiled wave reads its cells' normals from the tile, any other wave computes them)
     constexpr bool kCoop = PATH && EULER && MAXV == 7 && !RCache<MAXV, PATH, EULER>::value && MOPS_CPOLY &&
                            MOPS_COOP_PE;
-    constexpr bool kRC = RCache<MAXV, PATH, EULER>::value, kNrm = LdsNormals<MAXV, PATH, EULER>::value && !kCoop;
-    __shared__ double s_nrm[kNrm ? 3 * kNrmSlots(MAXV) * kTrajBlock : 1];  // per-lane edge normals (Cell::nrm)
+    constexpr bool kRC = RCache<MAXV, PATH, EULER>::value, kNrm = LdsNormals<MAXV, PATH, EULER>::value;
+    // per-lane edge normals (Cell::nrm); in the cooperative kernel the same LDS holds either them (a wave in
+    // lane-normal mode, c.lds_n) or the wave's tile
+    constexpr int kNrmD = 3 * kNrmSlots(MAXV) * kTrajBlock, kTileD = 2 * MOPS_COOP_G * kTilePieces;
+    __shared__ double s_nrm[kNrm ? (kCoop && kTileD > kNrmD ? kTileD : kNrmD) : 1];
     c.nrm = s_nrm + threadIdx.x;
+    c.lds_n = kNrm && !kCoop;  // (the cooperative kernel starts in tile mode)
     constexpr bool kPairT = (kNrm || kCoop) && (PATH ? MOPS_PAIR_TEST_P : MOPS_PAIR_TEST);  // (load_cell resets it)
     __shared__ double s_pr2[kPairT ? (MOPS_LDS_COMPACT ? 4 : 5) * kTrajBlock : 1];  // per-lane pair test (Cell::pr2, dev::walk)
     __shared__ float s_rb2[kPairT && MOPS_LDS_COMPACT ? kTrajBlock : 1];
     c.pr2 = s_pr2 + threadIdx.x;
     c.rb2 = s_rb2 + (kPairT && MOPS_LDS_COMPACT ? threadIdx.x : 0);
-    __shared__ double2 s_tile[kCoop ? MOPS_COOP_G * kTilePieces : 1];
+    double2* s_tile = reinterpret_cast<double2*>(s_nrm);
     __shared__ uint4 s_hdr[kCoop ? MOPS_COOP_G * (kTileHdr / 4) : 1];
     const int C = a.C;
     // next recording step (the smallest j >= step_begin with (j+1) % rec_period == 0) and its
@@ -1502,7 +1513,7 @@ __global__ void __launch_bounds__(kTrajBlock, (TrajWaves<MAXV, PATH, EULER>::val
         MOPS_MARK(100);
         if (step == 0) {  // first_loop (:892-901)
             if (cell < 0 || cell >= C) { died = 0; break; }
-            dev::load_cell<MAXV, kRC, kNrm, kPairT>(c, cell, a.cellrec, a.vxyz, a.mono0, a.mono1, a.cxyz, a.cpoly);
+            dev::load_cell<MAXV, kRC, kNrm, kPairT, kCoop>(c, cell, a.cellrec, a.vxyz, a.mono0, a.mono1, a.cxyz, a.cpoly, a.cnrm);
             double* r0 = a.rec;
             r0[0 * a.rec_stride + pid] = x;
             r0[1 * a.rec_stride + pid] = y;
@@ -1513,7 +1524,7 @@ __global__ void __launch_bounds__(kTrajBlock, (TrajWaves<MAXV, PATH, EULER>::val
             rec0 = true;
         } else {  // one-hop nearest-centre walk (:902-922)
             if (cell < 0 || cell >= C) { died = (int)step; break; }
-            if (c.id != cell) dev::load_cell<MAXV, kRC, kNrm, kPairT>(c, cell, a.cellrec, a.vxyz, a.mono0, a.mono1, a.cxyz, a.cpoly);
+            if (c.id != cell) dev::load_cell<MAXV, kRC, kNrm, kPairT, kCoop>(c, cell, a.cellrec, a.vxyz, a.mono0, a.mono1, a.cxyz, a.cpoly, a.cnrm);
             // Exact shortcut: inside the stay ball around the anchor every
             // neighbour is strictly farther than c by more than rounding, so
             // the reference's argmin (c listed last, strict <) keeps c (dev::walk).
@@ -1531,7 +1542,7 @@ __global__ void __launch_bounds__(kTrajBlock, (TrajWaves<MAXV, PATH, EULER>::val
             if (walking) {
                 cell = dev::walk<MAXV, kPairT>(c, cell, x, y, z, a.cellrec, a.cxyz, C);
                 loading = c.id != cell;
-                if (c.id != cell) dev::load_cell<MAXV, kRC, kNrm, kPairT>(c, cell, a.cellrec, a.vxyz, a.mono0, a.mono1, a.cxyz, a.cpoly);
+                if (c.id != cell) dev::load_cell<MAXV, kRC, kNrm, kPairT, kCoop>(c, cell, a.cellrec, a.vxyz, a.mono0, a.mono1, a.cxyz, a.cpoly, a.cnrm);
             }
             {
                 const unsigned long long bw = __ballot(walking), bl = __ballot(loading), ba = __ballot(1);
@@ -1566,7 +1577,7 @@ __global__ void __launch_bounds__(kTrajBlock, (TrajWaves<MAXV, PATH, EULER>::val
 #endif
                 cell = dev::walk<MAXV, kPairT>(c, cell, x, y, z, a.cellrec, a.cxyz, C);
                 if (c.id != cell) MOPS_CNT(5, 1);
-                if (c.id != cell) dev::load_cell<MAXV, kRC, kNrm, kPairT>(c, cell, a.cellrec, a.vxyz, a.mono0, a.mono1, a.cxyz, a.cpoly);
+                if (c.id != cell) dev::load_cell<MAXV, kRC, kNrm, kPairT, kCoop>(c, cell, a.cellrec, a.vxyz, a.mono0, a.mono1, a.cxyz, a.cpoly, a.cnrm);
             }
 #endif
         }
@@ -1582,7 +1593,10 @@ __global__ void __launch_bounds__(kTrajBlock, (TrajWaves<MAXV, PATH, EULER>::val
             // particle-day at config 3.  Any change regroups the wave and refills the whole tile.
             const int hk = ((hint0 + 1) << 16) | ((hint1 + 1) << 8);  // (hints >= -1, < 2^7)
             const bool moved = (cell != tcell) | (hk != (tkey & ~0xff));
-            if (__ballot(moved) != 0ull || !have_tile) {
+            // tile mode: regroup when a lane moved; lane-normal mode (a wave with too many groups): try
+            // again every 64 steps
+            const bool regroup = c.lds_n ? ((step - a.step_begin) & 63) == 0 : (__ballot(moved) != 0ull || !have_tile);
+            if (regroup) {
                 // groups of live lanes with equal (cell, hint0, hint1), found leader by leader with
                 // scalar readlanes + ballots; more than MOPS_COOP_G groups: the lanes gather themselves
                 const uint64_t act = __ballot(1);
@@ -1683,10 +1697,17 @@ __global__ void __launch_bounds__(kTrajBlock, (TrajWaves<MAXV, PATH, EULER>::val
                         }
                     }
                     __builtin_amdgcn_wave_barrier();
+                    c.lds_n = false;  // (the tile overwrote the lane normals)
+                } else if (!c.lds_n) {  // tile mode -> lane-normal mode: each lane's normals of its cell
+#pragma unroll
+                    for (int k = 0; k < 3 * kNrmSlots(MAXV); ++k)
+                        c.nrm[k * kTrajBlock] = a.cnrm[(int64_t)cell * kCellNrm + k];
+                    c.lds_n = true;
+                    __builtin_amdgcn_wave_barrier();
                 }
                 tcell = cell;
                 tkey = hk | (coop ? g : 0xff);
-                have_tile = true;
+                have_tile = coop;
                 coop_prev = coop;
             } else {
                 coop = coop_prev;

@@ -42,6 +42,17 @@ mul, nm = total_any("SQ_INSTS_VALU_MUL_F64")
 fma, nfm = total_any("SQ_INSTS_VALU_FMA_F64")
 if na and nm and nfm:
     rec["fp64_flops_per_unit"] = 64.0 * (add + mul + 2.0 * fma) / units
+# the memory-return view (tools/pmc_td.sh counters in the profile's td/ pass): vector-L1 tag accesses
+# (64 B each: tools/membench.hip, mb_l1_x4), L1 -> L2 read requests (128 B each) and TD busy cycles
+tcp, nt = total("TCP_TOTAL_CACHE_ACCESSES_sum", "td")
+tcc, _ = total("TCP_TCC_READ_REQ_sum", "td")
+tdb, _ = total("TD_TD_BUSY_sum", "td")
+grbm, ng = total("GRBM_GUI_ACTIVE", "td")
+if nt:
+    rec["tcp_accesses_per_unit"] = tcp / units
+    rec["l1_to_l2_requests_per_unit"] = tcc / units
+    if grbm > 0:
+        rec["td_busy"] = (tdb / 256.0) / (grbm / 8.0)
 recs = []
 if os.path.exists(dst):
     old = json.load(open(dst))
