@@ -168,9 +168,10 @@ class MPASOReader:
         nc.close()
         return r
 
-    # ---- MPASOReader::readSolData (MPASOReader.cpp:171-245)
     @staticmethod
-    def readSolData(yaml_path: str, data_name: str, timestep: int = 0) -> "MPASOReader":
+    def _locate(yaml_path: str, data_name: str, timestep: int):
+        """(stream, data substream, file of the global step, record in it, the named file) -- the ftk
+        stream's global step = first_timestep_per_file[file with data_name] + timestep."""
         if timestep < 0:
             raise ValueError(f"[MPASOReader]::Error: Invalid timestep index {timestep}")
         stream = _load_yaml(yaml_path)
@@ -193,12 +194,34 @@ class MPASOReader:
         j = int(np.searchsorted(first, index, side="right") - 1)
         if j < 0 or index - first[j] >= counts[j]:
             raise IndexError(f"[MPASOReader]: global step {index} beyond the data files")
-        nc = NcFile(files[j])
-        gs = _read_group(nc, sub, index - int(first[j]))
+        return stream, sub, files[j], index - int(first[j]), files[fi]
+
+    @staticmethod
+    def readTimeStamp(yaml_path: str, data_name: str, timestep: int = 0) -> str:
+        """The snapshot's xtime alone (what MPASOSolution::getTimeStamp returns after readSolData), without
+        reading its fields: the chain needs every pair's gap before it derives any field."""
+        _, sub, path, rec, _ = MPASOReader._locate(yaml_path, data_name, timestep)
+        names = next((v.get("possible_names") or [v["name"]] for v in sub.get("vars", []) or []
+                      if v["name"] == "xtime"), ["xtime", "xtime_startMonthly", "xtime_startDaily"])
+        nc = NcFile(path)
+        try:
+            found = next((c for c in names if nc.info(c) is not None), None)
+            if found is None:
+                return ""
+            return bytes(np.asarray(nc.read(found, rec), dtype=np.uint8).reshape(-1)).decode(errors="replace")
+        finally:
+            nc.close()
+
+    # ---- MPASOReader::readSolData (MPASOReader.cpp:171-245)
+    @staticmethod
+    def readSolData(yaml_path: str, data_name: str, timestep: int = 0) -> "MPASOReader":
+        stream, sub, path, rec, named = MPASOReader._locate(yaml_path, data_name, timestep)
+        nc = NcFile(path)
+        gs = _read_group(nc, sub, rec)
         nc.close()
         r = MPASOReader(yaml_path)
         r.mTimesteps = int(timestep)
-        r.mDataName = os.path.splitext(os.path.basename(files[fi]))[0]
+        r.mDataName = os.path.splitext(os.path.basename(named))[0]
         r.mFolderName = stream.get("path_prefix", "")
 
         def d(name):

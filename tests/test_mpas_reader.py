@@ -123,6 +123,9 @@ def test_mpas_reader_classic(engine_lib, tmp_path, version):
     s = MPASOReader.readSolData(str(y), "0001-02-01", 0)
     assert s.mVertLevels == mesh.nVertLevels and s.mVertLevelsP1 == mesh.nVertLevels + 1
     assert s.mTimeStamp.startswith("0003-01-01_00:00:00")
+    # the xtime alone (MOPSPathline reads every snapshot's stamp before deriving any field)
+    assert MPASOReader.readTimeStamp(str(y), "0001-02-01", 0) == s.mTimeStamp
+    assert MPASOReader.readTimeStamp(str(y), "0001-01-01", 1).startswith("0002-01-01_00:00:00")
     assert np.array_equal(s.cellLayerThickness_vec, snaps[2].layerThickness)
     assert np.array_equal(s.cellZonalVelocity_vec, snaps[2].zonalVelocity)
     assert np.array_equal(s.cellVertVelocity_vec, snaps[2].vertVelocityTop)
