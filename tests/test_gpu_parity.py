@@ -217,17 +217,25 @@ def test_pathline_parity(dev_small, ref_small, small_case, oracle_lib, method):
     print(f"bit-exact points: {exact:.4f}")
 
 
-def test_pathline_cooperative_waves(dev_small, ref_small, small_case, oracle_lib):
+@pytest.mark.parametrize("variant", ["forward", "backward", "zlevel"])
+def test_pathline_cooperative_waves(gpu, engine_lib, dev_small, ref_small, small_case, oracle_lib, variant):
     """Pathline Euler waves that share cells (config 3's density: ~40 particles per cell) take the
-    cooperative path -- each group's polygon and hinted-layer records loaded once into the wave's LDS
-    tile (traj_kernel, MOPS_COOP_PE).  Dense cells with one or two depth groups (one or two
-    (cell, layer) groups per cell, so waves with 1..4 groups: tiled and not), seeds on land (dead at
-    step 0), particles dying later, and a partial last wave -- bit-exact against the oracle."""
+    cooperative path -- each group's polygon, edge normals and hinted-layer records loaded once into the
+    wave's LDS tile and kept until a lane's cell or layer changes (traj_kernel, MOPS_COOP_PE); waves
+    with more than 7 groups switch to per-lane normals.  Dense cells with one or two depth groups, seeds
+    on land (dead at step 0), particles dying later, a partial last wave; forward, backward (dt < 0),
+    and MPAS z-level columns (partial bottom cells: hint misses change the groups) -- bit-exact
+    against the oracle."""
     from mops_amd import synth
-    from mops_amd.engine import TrajectoryConfig, run_trajectories
+    from mops_amd.engine import DeviceField, TrajectoryConfig, run_trajectories
     mesh, _, _ = small_case
     dm, f0, f1 = dev_small
     r0, r1 = ref_small
+    if variant == "zlevel":
+        z0 = synth.make_snapshot(mesh, timestep=0, topography="zlevel")
+        z1 = synth.make_snapshot(mesh, timestep=1, phase=0.35, topography="zlevel")
+        f0, f1 = DeviceField.from_snapshot(dm, z0), DeviceField.from_snapshot(dm, z1)
+        r0, r1 = oracle_lib.preprocess(mesh, z0), oracle_lib.preprocess(mesh, z1)
     rng = np.random.default_rng(41)
     cc = np.asarray(mesh.cellCoord, dtype=np.float64).reshape(-1, 3)
     cells = rng.choice(mesh.nCells, 14, replace=False)
@@ -239,16 +247,20 @@ def test_pathline_cooperative_waves(dev_small, ref_small, small_case, oracle_lib
         p = u + (jit - np.outer(jit @ u, u)) / 6.371e6
         seeds.append(p / np.linalg.norm(p, axis=1, keepdims=True) * 6.37101e6)
         d = np.full(k, 300.0) if j < 7 else np.where(np.arange(k) % 2 == 0, 300.0, 1100.0)
+        if variant == "zlevel":  # around the local bottom of the shallowest columns (1500-4000 m)
+            d = np.where(np.arange(k) % 3 == 0, 1450.0 + 10.0 * j, d)
         depths.append(d)
     land = synth.uniform_band_seeds(400, seed=3)
     seeds.append(land[:37]); depths.append(np.full(37, 500.0))
     seeds = np.concatenate(seeds); depths = np.concatenate(depths).astype(np.float32)
-    cfg = TrajectoryConfig(deltaT=120, simulationDuration=43200, recordT=3600, depth=0.0, method=1)
+    back = variant == "backward"
+    cfg = TrajectoryConfig(deltaT=120, simulationDuration=43200, recordT=3600, depth=0.0, method=1,
+                           direction=1 if back else 0)
     got = run_trajectories(dm, f0, f1, cfg, seeds, depths=depths)
     ref = oracle_lib.run(mesh, r0, r1, seeds, depths=depths, delta_t=120, duration=43200, record_t=3600,
-                         euler=True, cells=got["cells"])
+                         euler=True, backward=back, cells=got["cells"])
     assert len(seeds) % 64 != 0
-    assert_lines_match(got, ref, "pathline cooperative waves")
+    assert_lines_match(got, ref, f"pathline cooperative waves ({variant})")
     assert (ref["death"] >= 0).any() and (ref["death"] < 0).sum() > len(seeds) // 2
 
 

@@ -8,16 +8,16 @@ export TMPDIR=/tmp
 # the counter passes must see only the measured workload's kernels (bench.py's RK4 companion off)
 export MOPS_BENCH_NO_RK4=1
 timeout -k 10 600 python3 bench.py ${BENCH_ARGS:-} > "$out/bench.json" 2> "$out/bench.err" || { echo "bench failed"; exit 1; }
-timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$out/stats" -o p -- \
+timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d "$out/stats" -o p -- \
     python3 bench.py --no-cpu-baseline ${BENCH_ARGS:-} > "$out/stats.log" 2>&1 || { echo "stats failed"; exit 1; }
-timeout -k 5 150 rocprofv3 --pmc FETCH_SIZE --kernel-include-regex traj_kernel --output-format csv -d "$out/fetch" -o p -- \
+timeout -k 5 300 rocprofv3 --pmc FETCH_SIZE --kernel-include-regex traj_kernel --output-format csv -d "$out/fetch" -o p -- \
     python3 bench.py --no-cpu-baseline --steps 1 --warmup 0 ${BENCH_ARGS:-} > "$out/fetch.log" 2>&1 || { echo "fetch failed"; exit 1; }
-timeout -k 5 150 rocprofv3 --pmc WRITE_SIZE --kernel-include-regex traj_kernel --output-format csv -d "$out/write" -o p -- \
+timeout -k 5 300 rocprofv3 --pmc WRITE_SIZE --kernel-include-regex traj_kernel --output-format csv -d "$out/write" -o p -- \
     python3 bench.py --no-cpu-baseline --steps 1 --warmup 0 ${BENCH_ARGS:-} > "$out/write.log" 2>&1 || { echo "write failed"; exit 1; }
-timeout -k 5 150 rocprofv3 --pmc TD_TD_BUSY_sum GRBM_GUI_ACTIVE TCP_TOTAL_CACHE_ACCESSES_sum TCP_TCC_READ_REQ_sum \
+timeout -k 5 300 rocprofv3 --pmc TD_TD_BUSY_sum GRBM_GUI_ACTIVE TCP_TOTAL_CACHE_ACCESSES_sum TCP_TCC_READ_REQ_sum \
     --kernel-include-regex traj_kernel --output-format csv -d "$out/td" -o p -- \
     python3 bench.py --no-cpu-baseline --steps 1 --warmup 0 ${BENCH_ARGS:-} > "$out/td.log" 2>&1 || { echo "td failed"; exit 1; }
-timeout -k 5 150 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_VALU_ADD_F64 SQ_INSTS_VALU_MUL_F64 SQ_INSTS_VALU_FMA_F64 \
+timeout -k 5 300 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_VALU_ADD_F64 SQ_INSTS_VALU_MUL_F64 SQ_INSTS_VALU_FMA_F64 \
     SQ_INSTS_VMEM_RD SQ_INSTS_LDS SQ_INSTS_SALU --kernel-include-regex traj_kernel --output-format csv -d "$out/pmc" -o p -- \
     python3 bench.py --no-cpu-baseline --steps 1 --warmup 0 ${BENCH_ARGS:-} > "$out/pmc.log" 2>&1 || { echo "pmc failed"; exit 1; }
 echo "profile ok"
