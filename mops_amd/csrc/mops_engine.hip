@@ -1488,7 +1488,7 @@ __global__ void __launch_bounds__(kTrajBlock, (TrajWaves<MAXV, PATH, EULER>::val
     // per-lane edge normals (Cell::nrm); in the cooperative kernel the same LDS holds either them (a wave in
     // lane-normal mode, c.lds_n) or the wave's tile
     constexpr int kNrmD = 3 * kNrmSlots(MAXV) * kTrajBlock, kTileD = 2 * MOPS_COOP_G * kTilePieces;
-    __shared__ double s_nrm[kNrm ? (kCoop && kTileD > kNrmD ? kTileD : kNrmD) : 1];
+    __shared__ __attribute__((aligned(16))) double s_nrm[kNrm ? (kCoop && kTileD > kNrmD ? kTileD : kNrmD) : 1];
     c.nrm = s_nrm + threadIdx.x;
     c.lds_n = kNrm && !kCoop;  // (the cooperative kernel starts in tile mode)
     constexpr bool kPairT = (kNrm || kCoop) && (PATH ? MOPS_PAIR_TEST_P : MOPS_PAIR_TEST);  // (load_cell resets it)
