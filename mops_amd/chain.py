@@ -237,8 +237,9 @@ class PathlineChain:
                         e0 = torch.cuda.Event(enable_timing=True); e1 = torch.cuda.Event(enable_timing=True)
                         e0.record(cs)
                     if reorder and s0 > 0:
-                        # the slots written so far: record 0's step-0 part .. the last completed record
-                        ps.reorder(stream=cs.cuda_stream, records_written=min(cfg.n_records, s0 // period + 1))
+                        # every record slot moves with its particle: a particle that died earlier in the
+                        # pair already holds the reference's zeros in its later slots
+                        ps.reorder(stream=cs.cuda_stream)
                     ps.advance(front, back, s0, min(s0 + seg, cfg.n_steps), stream=cs.cuda_stream)
                     if timing is not None:
                         e1.record(cs)

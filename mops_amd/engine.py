@@ -300,8 +300,9 @@ class ParticleSet:
 
     def reorder(self, stream=None, records_written: int | None = None):
         """Locality order of the particles by their current cell (mops_order_particles), applied by permuting
-        the SoA state (and the records already written: all slots, or the first ``records_written`` --
-        the launches from the current step write every later slot) so slot s holds particle ids[s]."""
+        the SoA state (and the records once written: every slot -- a particle that died already holds
+        the reference's zeros in its later slots -- or the first ``records_written`` when no particle can
+        have died yet) so slot s holds particle ids[s]."""
         L.check(L.load().mops_order_particles(self.mesh.handle, self.n, C.c_void_p(self.cell.data_ptr()),
                                               C.c_void_p(self.order.data_ptr()), _stream_handle(stream)),
                 "mops_order_particles")
