@@ -105,7 +105,7 @@ inline int rec_ints_for(int maxv) { return ((1 + 2 * maxv) + 3) / 4 * 4; }
 #define MOPS_COOP_PE 1
 #endif
 #ifndef MOPS_GR_COOP
-#define MOPS_GR_COOP 1  // level-pair records per LDS round trip in the tile instantiations
+#define MOPS_GR_COOP 2  // level-pair records per LDS round trip in the tile instantiations (1: +1%, 3: +7%)
 #endif
 #ifndef MOPS_COOP_R
 #define MOPS_COOP_R 12  // tile pieces per live lane at most (fewer live lanes: the lanes gather themselves)
@@ -1353,6 +1353,8 @@ struct TrajArgs {
     const int* __restrict__ n_live;  // device count of leading live slots (compaction), NULL = all n
     const double4* __restrict__ cpoly;  // per-cell rotated polygon + Wachspress B_i (mops_mesh::d_cpoly)
     const double* __restrict__ cnrm;    // per-cell edge normals (mops_mesh::d_cnrm; NULL past maxEdges 7)
+    const int* __restrict__ coop_sel;   // per-launch device flag: 1 = the cooperative instantiation runs, 0 = the
+                                        // plain one (the other exits at once); NULL = no selection
     double* px; double* py; double* pz;
     float* depth;
     int* cell;
@@ -1430,8 +1432,9 @@ struct TrajWaves {
     static constexpr int value = MAXV <= 7 ? base : (EULER ? 2 : 1);
 };
 
-template <int MAXV, bool PATH, bool EULER>
+template <int MAXV, bool PATH, bool EULER, bool COOP = false>
 __global__ void __launch_bounds__(kTrajBlock, (TrajWaves<MAXV, PATH, EULER>::value)) traj_kernel(TrajArgs a) {
+    if (a.coop_sel && ((*a.coop_sel != 0) != COOP)) return;  // the other instantiation runs this launch
     // XCD-aware mapping: blocks b, b+8, ... share an XCD (L2); give each XCD a
     // contiguous range of the locality-ordered particles (bijective remap)
     // After a compaction only the first *n_live slots hold live particles: the remap then spreads
@@ -1482,7 +1485,7 @@ __global__ void __launch_bounds__(kTrajBlock, (TrajWaves<MAXV, PATH, EULER>::val
     c.V = a.V;
     // cooperative waves (see kTilePieces): the wave's LDS tile and its group headers; their kernel keeps no
     // per-lane normals (a tiled wave reads its cells' normals from the tile, any other wave computes them)
-    constexpr bool kCoop = PATH && EULER && MAXV == 7 && !RCache<MAXV, PATH, EULER>::value && MOPS_CPOLY &&
+    constexpr bool kCoop = COOP && PATH && EULER && MAXV == 7 && !RCache<MAXV, PATH, EULER>::value && MOPS_CPOLY &&
                            MOPS_COOP_PE;
     constexpr bool kRC = RCache<MAXV, PATH, EULER>::value, kNrm = LdsNormals<MAXV, PATH, EULER>::value;
     // per-lane edge normals (Cell::nrm); in the cooperative kernel the same LDS holds either them (a wave in
@@ -2922,11 +2925,51 @@ int64_t gcd64(int64_t a, int64_t b) {
     return a;
 }
 
+// Which pathline-Euler instantiation runs a launch: the cooperative tile pays where a wave's lanes
+// share few cells (configs 3 and 5: 40+ particles per cell), the plain kernel where they do not (config
+// 4: ~3 per cell, ~20 cells per wave).  One block samples up to 4096 of the launch's 64-slot waves in
+// the current (locality) order, counts the runs of equal cells in each, and writes flag = 1 when the
+// mean is at most MOPS_COOP_CELLS -- on the device, so the host never waits.
+#ifndef MOPS_COOP_CELLS
+#define MOPS_COOP_CELLS 6
+#endif
+__global__ void __launch_bounds__(256) coop_select_kernel(int64_t n, const int* __restrict__ cell,
+                                                          const int* __restrict__ n_live, int* __restrict__ flag) {
+    __shared__ unsigned long long runs[256];
+    int64_t m = n;
+    if (n_live) m = min<int64_t>(m, (int64_t)*n_live);
+    const int64_t waves = (m + 63) / 64;
+    const int64_t S = waves < 4096 ? waves : 4096;
+    unsigned long long r = 0;
+    for (int64_t j = threadIdx.x; j < S; j += blockDim.x) {
+        const int64_t w = j * waves / S, lo = 64 * w, hi = min<int64_t>(m, lo + 64);
+        int prev = cell[lo];
+        r += 1;
+        for (int64_t i = lo + 1; i < hi; ++i) {
+            const int c = cell[i];
+            r += (c != prev);
+            prev = c;
+        }
+    }
+    runs[threadIdx.x] = r;
+    __syncthreads();
+    for (int k = blockDim.x / 2; k > 0; k >>= 1) {
+        if ((int)threadIdx.x < k) runs[threadIdx.x] += runs[threadIdx.x + k];
+        __syncthreads();
+    }
+    if (threadIdx.x == 0) *flag = (S > 0 && runs[0] <= (unsigned long long)MOPS_COOP_CELLS * (unsigned long long)S) ? 1 : 0;
+}
+
 template <int MAXV>
 void launch_traj(const TrajArgs& a, bool path, bool euler, hipStream_t s) {
     const unsigned g = (unsigned)((a.n + kTrajBlock - 1) / kTrajBlock);
     if (path) {
-        if (euler) traj_kernel<MAXV, true, true><<<g, kTrajBlock, 0, s>>>(a);
+        if (euler) {
+            if constexpr (MAXV == 7) {  // both instantiations; a.coop_sel lets exactly one of them run
+                if (a.coop_sel) traj_kernel<MAXV, true, true, true><<<g, kTrajBlock, 0, s>>>(a);
+            }
+            traj_kernel<MAXV, true, true><<<g, kTrajBlock, 0, s>>>(a);
+        }
         else traj_kernel<MAXV, true, false><<<g, kTrajBlock, 0, s>>>(a);
     } else {
         if (euler) traj_kernel<MAXV, false, true><<<g, kTrajBlock, 0, s>>>(a);
@@ -3724,6 +3767,14 @@ mops_status mops_traj_advance(const mops_mesh* mesh, const mops_field* front, co
     a.rec_stride = record_stride;
     const bool euler = (cfg->method == MOPS_EULER);
     hipStream_t s = (hipStream_t)stream;
+    a.coop_sel = nullptr;
+    int* sel = nullptr;
+    if (MOPS_COOP_PE && back && euler && mesh->maxv == 7 && !p->d_order) {
+        // a per-launch flag (stream-ordered allocation: concurrent launches on other streams keep their own)
+        HIP_TRY(hipMallocAsync(reinterpret_cast<void**>(&sel), sizeof(int), s));
+        coop_select_kernel<<<1, 256, 0, s>>>(p->n, p->d_cell, p->d_n_live, sel);
+        a.coop_sel = sel;
+    }
     switch (mesh->maxv) {
         case 7: launch_traj<7>(a, back != nullptr, euler, s); break;
 #if !defined(MOPS_ONLY7)  // experiment builds: MAXV 7 instantiations only
@@ -3733,6 +3784,7 @@ mops_status mops_traj_advance(const mops_mesh* mesh, const mops_field* front, co
         default: return fail(MOPS_ERR_UNSUPPORTED, "experiment build: MAXV 7 only");
 #endif
     }
+    if (sel) HIP_TRY(hipFreeAsync(sel, s));
     HIP_TRY(hipGetLastError());
     return MOPS_OK;
 }

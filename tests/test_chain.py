@@ -168,3 +168,23 @@ def test_chain_overlap_stream_matches_serial(engine_lib, gpu, small_case):
         assert len(rec.pool) == (3 if overlap else 2)
     for k in results[0]:
         assert np.array_equal(results[0][k], results[1][k]), k
+
+
+@pytest.mark.gpu
+def test_chain_resorts_after_deaths(engine_lib, oracle_lib, gpu, small_case):
+    """Launches of 5 steps with a locality re-sort between them (PathlineChain segment_steps), RK4 so that
+    particles die inside a pair (quirk Q1): a dead particle's zeroed later record slots move with it, and
+    the lines equal the oracle chain's bit for bit."""
+    from mops_amd import synth
+    from mops_amd.chain import PathlineChain, snapshot_field_factory
+    from mops_amd.engine import DeviceMesh
+    mesh, _, _ = small_case
+    snaps = [synth.make_snapshot(mesh, timestep=t, phase=0.35 * t) for t in range(3)]
+    seeds = synth.uniform_band_seeds(300, seed=17)
+    dm = DeviceMesh.from_mesh(mesh)
+    chain = PathlineChain(dm, snapshot_field_factory(dm, lambda i: snaps[i]), len(snaps), gap_seconds=[43200, 21600])
+    got = chain.run(seeds, depth=200.0, method=0, delta_t=600, record_t=3600, segment_steps=5)
+    ref = oracle_chain(oracle_lib, mesh, snaps, seeds, 200.0, None, [43200, 21600], 600, 3600, euler=False)
+    assert (np.linalg.norm(ref["points"], axis=-1) == 0).any(), "the case should leave dead particles' zero slots"
+    for k in ("points", "velocity", "lastPoint"):
+        assert np.array_equal(got[k].cpu().numpy(), ref[k]), k
