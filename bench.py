@@ -692,7 +692,7 @@ def main_chain(args, mesh, dev, world, rank):
     t_start = [time.perf_counter()]
 
     def on_pair(p, last, ps):
-        if rank == 0 and args.pairs > 7:  # progress for long chains (stderr)
+        if rank == 0 and (args.pairs > 7 or world > 1):  # progress for long chains and multi-rank runs (stderr)
             print(f"[bench] pair {p + 1}/{args.pairs} enqueued at {time.perf_counter() - t_start[0]:.1f} s",
                   file=sys.stderr, flush=True)
         if gather_records:  # the pair's trajectory records (+ seeds, slot ids) on every rank
@@ -720,6 +720,9 @@ def main_chain(args, mesh, dev, world, rank):
         compute.synchronize(); comm.synchronize()
         return res
 
+    if rank == 0:
+        print(f"[bench] config {args.config}: setup done, {args.warmup} warmup + {args.steps} timed chains",
+              file=sys.stderr, flush=True)
     for _ in range(args.warmup):
         one_call(False)
     if world > 1:
@@ -727,8 +730,11 @@ def main_chain(args, mesh, dev, world, rank):
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     attempted = 0
-    for _ in range(args.steps):
+    for k in range(args.steps):
         attempted += int(one_call(True)["attempted"].item())
+        if rank == 0:
+            print(f"[bench] timed chain {k + 1}/{args.steps} done at {time.perf_counter() - t0:.1f} s", file=sys.stderr,
+                  flush=True)
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()

@@ -146,6 +146,11 @@ class RecordGather:
         self.aux = [torch.zeros((4, self.stride), dtype=torch.float64, device=dev) for _ in range(2)]
         per_rec = self.world * 6 * self.stride * 8
         self.chunk = self.shape[0] if not max_bytes else max(1, min(self.shape[0], int(max_bytes) // per_rec))
+        if self.world > 1:  # every rank must issue the same collectives: the smallest chunk of all ranks
+            t = torch.tensor([self.chunk], dtype=torch.int64,
+                             device=dev if (backend == "nccl" and self.cuda) else "cpu")
+            dist.all_reduce(t, op=dist.ReduceOp.MIN, group=group)
+            self.chunk = int(t.item())
         self.on_chunk = on_chunk
         self.gathered = torch.empty((self.world, self.chunk, 6, self.stride), dtype=torch.float64, device=dev)
         self.gathered_aux = torch.empty((self.world, 4, self.stride), dtype=torch.float64, device=dev)
