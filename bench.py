@@ -759,7 +759,10 @@ def main_chain(args, mesh, dev, world, rank):
     mesh_class = "EC30to60" if args.config == 3 else "oRRS18to6"
     from mops_amd.chain import REORDER_SECONDS
     seg_key = args.segment if args.segment > 0 else min(gaps[0] // args.dt, REORDER_SECONDS // args.dt)
-    roof = roofline_block(f"traj_kernel<7,true,{str(args.method == 'euler').lower()}> (pathline {args.method})",
+    kname = (f"traj_kernel<7,true,true,true|false> (pathline euler: the cooperative-tile instantiation where the "
+             f"launch's sampled cells per wave are <= 6, else the plain one; both dispatched, the other exits at once)"
+             if args.method == "euler" else "traj_kernel<7,true,false> (pathline rk4)")
+    roof = roofline_block(kname,
                           avg_kernel_s, psteps_per_launch, B,
                           f"{mesh_class.lower()}_chain{args.config}_{args.method}_{args.particles}_seg{seg_key}")
     cpu = None
