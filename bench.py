@@ -86,7 +86,8 @@ def parse(argv=None):
                         "partial bottom cells and zero-thickness inactive levels")
     p.add_argument("--side-cus", type=int, default=0,
                    help="configs 4/5: CUs reserved for a side stream that generates and derives snapshot p+2 while "
-                        "pair p computes on the others (three field buffers); 0 = off (two buffers, derivation "
+                        "pair p computes on the others (three field buffers); -1 = the same on an unmasked side "
+                        "stream (its kernels share every CU with the trajectory launch); 0 = off (two buffers, derivation "
                         "between pairs, the default: measured slower, DESIGN.md section 3.3)")
     p.add_argument("--compact", choices=["auto", "on", "off"], default="auto",
                    help="config 2: re-sort each particle part with its dead particles last between step chunks "
@@ -236,6 +237,32 @@ def l1_block(key: str, unit_s: float):
             "source": src + " TCP_TOTAL_CACHE_ACCESSES_sum x 64 B, TD_TD_BUSY_sum / 256 over GRBM_GUI_ACTIVE / 8"}
 
 
+def valu_block(key: str):
+    """The VALU-issue view: how much of the SIMDs' cycles the kernel's vector instructions hold, from the same
+    profile (tools/make_traffic.py valu_issue_model: FP64 add/mul/fma 4 SIMD-cycles per wave64, other VALU 2;
+    tools/merge_issue.py valu_busy: rocprof's VALUBusy from SQ_ACTIVE_INST_VALU)."""
+    e, src = measured_entry(key)
+    if not e or e.get("valu_issue_model") is None:
+        return {"frac": None, "source": src}
+    return {"frac": e["valu_issue_model"], "valu_busy": e.get("valu_busy"), "salu_busy": e.get("salu_busy"),
+            "lds_busy": e.get("lds_busy"), "unit": "fraction of SIMD cycles",
+            "source": src + " SQ_INSTS_VALU{,_ADD_F64,_MUL_F64,_FMA_F64}: (4 x FP64 + 2 x other) / (1024 SIMDs x "
+                      "GRBM_GUI_ACTIVE / 8); valu_busy = SQ_ACTIVE_INST_VALU x 4 / 1024 / (GRBM_GUI_ACTIVE / 8)"}
+
+
+def limiter_text(l1: dict, valu: dict) -> str:
+    td, vf = l1.get("td_busy"), valu.get("frac")
+    if td is not None and vf is not None:
+        if td >= 0.8:
+            return (f"texture-data return of the per-lane gathers: TD {td:.0%} busy (l1_return); VALU issue "
+                    f"{vf:.0%} of SIMD cycles (valu_issue) -- DESIGN.md section 3")
+        return (f"VALU issue: the FP64 geometry holds {vf:.0%} of SIMD cycles by instruction count "
+                f"(rocprof VALUBusy {valu.get('valu_busy') or float('nan'):.0%}); TD {td:.0%} busy, DRAM far below "
+                "its peak -- DESIGN.md section 3")
+    return ("not DRAM: the texture-data return of the per-lane gathers (l1_return) together with FP64 VALU "
+            "issue and gather latency at 3 waves/SIMD (DESIGN.md section 3)")
+
+
 def roofline_block(kernel: str, avg_kernel_s: float, psteps_per_launch: float, B: float, traffic_key: str,
                    per: str = "launch") -> dict:
     """The bench line's roofline: HBM GB/s MEASURED by rocprofv3 PMC counters (per launch) over the
@@ -253,8 +280,8 @@ def roofline_block(kernel: str, avg_kernel_s: float, psteps_per_launch: float, B
         "frac": (achieved / PEAK_HBM_GBS) if achieved is not None else None,
         "traffic": traffic,
         "traffic_source": src,
-        "limiter": ("not DRAM: the texture-data return of the per-lane gathers (l1_return) together with FP64 VALU "
-                    "issue and gather latency at 3 waves/SIMD (DESIGN.md section 3)"),
+        "limiter": limiter_text(l1_block(traffic_key, avg_kernel_s), valu_block(traffic_key)),
+        "valu_issue": valu_block(traffic_key),
         "fp64_valu": fp64_block(traffic_key, avg_kernel_s),
         "l1_return": l1_block(traffic_key, avg_kernel_s),
         "traffic_correction": ("bytes = 2 x FETCH_SIZE + WRITE_SIZE: the gfx950 factor 1/2 holds for this kernel's "
@@ -649,9 +676,12 @@ def main_chain(args, mesh, dev, world, rank):
         recycler = DeviceFieldRecycler(dmesh, src)
         side_cus = args.side_cus or 0
         overlap = None
-        if side_cus > 0 and n_snap > 2:
+        if side_cus != 0 and n_snap > 2:
             from mops_amd.chain import cu_split_streams
-            compute_masked, overlap = cu_split_streams(dev, side_cus)
+            if side_cus > 0:
+                compute_masked, overlap = cu_split_streams(dev, side_cus)
+            else:
+                compute_masked, overlap = torch.cuda.Stream(dev), torch.cuda.Stream(dev)
             recycler.side = overlap  # snapshot generation runs there too
         # the field buffers (2, or 3 with the overlap stream) are allocated before the timed region
         # (hipMalloc of ~75 GB each is setup); every snapshot a call uses is still generated and
@@ -801,8 +831,12 @@ def main_chain(args, mesh, dev, world, rank):
                 "snapshot_times": [stamps[0], stamps[-1]], "pair_seconds": sorted(set(gaps)),
                 "records_per_pair": sorted({g // args.record for g in gaps}), "record_t": args.record,
                 "method": args.method, "parallelism": f"particle-shard x{world}",
-                "snapshot_overlap": (f"snapshot p+2 generated + derived on a {chain.overlap_stream_cus}-CU side stream "
-                                     "during pair p (3 field buffers)") if chain.overlap_stream is not None else "none",
+                "snapshot_overlap": (
+                    ((f"snapshot p+2 generated + derived on a {chain.overlap_stream_cus}-CU side stream"
+                      if chain.overlap_stream_cus > 0 else "snapshot p+2 generated + derived on an unmasked side stream")
+                     + " during pair p (3 field buffers)") if chain.overlap_stream is not None else
+                    "snapshot p+2 generated on a side stream beside pair p's launches, derived after pair p"
+                    if args.config in (4, 5) else "none (every snapshot derived before the timed region)"),
                 "record_gather": record_gather_text(world, args, per="pair", K=max(g // args.record for g in gaps),
                                                     collector=collector[0])},
             "nominal_particle_steps_per_call": n_all * n_steps,

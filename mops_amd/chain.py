@@ -206,8 +206,6 @@ class PathlineChain:
                     fields[p + 2] = self.make_field.refill(buf, p + 2, ov)
                     ready[p + 2] = torch.cuda.Event()
                     ready[p + 2].record(ov)
-            elif recycle and p + 2 < self.n_snapshots and hasattr(self.make_field, "prepare"):
-                self.make_field.prepare(p + 2)  # raw snapshot p+2 generated on a side stream during pair p
             if p + 1 in ready:
                 cs.wait_event(ready.pop(p + 1))  # pair p's back snapshot was derived on the overlap stream
             with torch.cuda.stream(cs):
@@ -228,6 +226,13 @@ class PathlineChain:
                 # a continuation pair: each particle's current cell is an exact-locate hint
                 ps.reseed(s, d, stream=cs.cuda_stream, hint_cells=(p > 0 and follow_last))
                 front, back = fields[p], fields[p + 1]
+                if (not overlap and recycle and p + 2 < self.n_snapshots
+                        and hasattr(self.make_field, "prepare")):
+                    # raw snapshot p+2 generated on a side stream beside pair p's first launch (started
+                    # earlier, its blocks would fill the GPU ahead of the reseed's small kernels)
+                    started = torch.cuda.Event()
+                    started.record(cs)
+                    self.make_field.prepare(p + 2, after=started)
                 if segment_steps < 0:
                     seg = max(1, REORDER_SECONDS // int(delta_t))
                 else:

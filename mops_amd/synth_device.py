@@ -111,11 +111,16 @@ class DeviceFieldRecycler:
         del snap
         return f
 
-    def prepare(self, i):
+    def prepare(self, i, after=None):
+        """``after``: an event the generation also waits for (the chain passes one recorded right before
+        a trajectory launch, so the generation runs beside that launch instead of in front of the
+        small kernels that precede it)."""
         torch = self.torch
         with torch.cuda.stream(self.side):
             if self.consumed is not None:
                 self.side.wait_event(self.consumed)  # the previous refill has read the raw set
+            if after is not None:
+                self.side.wait_event(after)
             self.raw = None
             self.raw = self.source.make(timestep=i, phase=self.phase * i)
             self.ready = torch.cuda.Event()

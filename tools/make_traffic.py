@@ -42,6 +42,7 @@ mul, nm = total_any("SQ_INSTS_VALU_MUL_F64")
 fma, nfm = total_any("SQ_INSTS_VALU_FMA_F64")
 if na and nm and nfm:
     rec["fp64_flops_per_unit"] = 64.0 * (add + mul + 2.0 * fma) / units
+valu, nv = total_any("SQ_INSTS_VALU")
 # the memory-return view (tools/pmc_td.sh counters in the profile's td/ pass): vector-L1 tag accesses
 # (64 B each: tools/membench.hip, mb_l1_x4), L1 -> L2 read requests (128 B each) and TD busy cycles
 tcp, nt = total("TCP_TOTAL_CACHE_ACCESSES_sum", "td")
@@ -53,6 +54,11 @@ if nt:
     rec["l1_to_l2_requests_per_unit"] = tcc / units
     if grbm > 0:
         rec["td_busy"] = (tdb / 256.0) / (grbm / 8.0)
+        if nv and na and nm and nfm:
+            # VALU issue model: a wave64 FP64 add/mul/fma holds its 32-wide SIMD 4 cycles (78.6 TF = 16 FP64 FMA
+            # lanes per SIMD-cycle), any other VALU 2 (MI355X_MICROARCH.md); against 1024 SIMDs x the cycles
+            f64 = add + mul + fma
+            rec["valu_issue_model"] = (4.0 * f64 + 2.0 * (valu - f64)) / units / (1024.0 * grbm / units / 8.0)
 recs = []
 if os.path.exists(dst):
     old = json.load(open(dst))

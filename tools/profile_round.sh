@@ -20,4 +20,9 @@ timeout -k 5 300 rocprofv3 --pmc TD_TD_BUSY_sum GRBM_GUI_ACTIVE TCP_TOTAL_CACHE_
 timeout -k 5 300 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_VALU_ADD_F64 SQ_INSTS_VALU_MUL_F64 SQ_INSTS_VALU_FMA_F64 \
     SQ_INSTS_VMEM_RD SQ_INSTS_LDS SQ_INSTS_SALU --kernel-include-regex traj_kernel --output-format csv -d "$out/pmc" -o p -- \
     python3 bench.py --no-cpu-baseline --steps 1 --warmup 0 ${BENCH_ARGS:-} > "$out/pmc.log" 2>&1 || { echo "pmc failed"; exit 1; }
+timeout -k 5 300 rocprofv3 --pmc SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_SCA SQ_ACTIVE_INST_VMEM SQ_ACTIVE_INST_LDS \
+    SQ_ACTIVE_INST_ANY SQ_WAVE_CYCLES SQ_BUSY_CYCLES GRBM_GUI_ACTIVE --kernel-include-regex traj_kernel --output-format csv \
+    -d "$out/issue" -o p -- python3 bench.py --no-cpu-baseline --steps 1 --warmup 0 ${BENCH_ARGS:-} > "$out/issue.log" 2>&1 \
+    || { echo "issue failed"; exit 1; }
+# then: tools/make_traffic.py $out KEY profiles/pmc_traffic.json UNITS && tools/merge_issue.py $out/issue KEY profiles/pmc_traffic.json
 echo "profile ok"
