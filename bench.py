@@ -84,6 +84,11 @@ def parse(argv=None):
     p.add_argument("--topography", choices=["sigma", "zlevel"], default="sigma",
                    help="config 2: synthetic vertical grid (synth.make_snapshot): 'zlevel' = MPAS-O z-levels with "
                         "partial bottom cells and zero-thickness inactive levels")
+    p.add_argument("--defer-lines", action="store_true",
+                   help="configs 3-5: assemble each pair's lines on a side stream beside the next pair "
+                        "(PathlineChain.run(defer_lines=True); not with record gathers). Off by default: measured "
+                        "neutral (config 3 3838/3846 vs 3829 ms, config 4 3119 vs 3120 ms per 6 pairs) -- the "
+                        "assembly's blocks take LDS and CU slots from the LDS-limited trajectory launch")
     p.add_argument("--side-cus", type=int, default=0,
                    help="configs 4/5: CUs reserved for a side stream that generates and derives snapshot p+2 while "
                         "pair p computes on the others (three field buffers); -1 = the same on an unmasked side "
@@ -714,6 +719,7 @@ def main_chain(args, mesh, dev, world, rank):
         if int(t[0].item()) != -int(t[1].item()):
             raise SystemExit("bench.py: ranks drew different particle counts")
     gather_records = world > 1 and args.gather == "records"
+    defer_lines = args.defer_lines and not gather_records  # (RecordGather reads the pair's slab in on_pair)
     gathered = torch.empty((world, n_pad, 3), dtype=torch.float64, device=dev) if world > 1 else None
     send = torch.zeros((n_pad, 3), dtype=torch.float64, device=dev) if world > 1 else None
     collector = [None]
@@ -746,7 +752,7 @@ def main_chain(args, mesh, dev, world, rank):
         res = chain.run(seeds, depth=args.depth, method=1 if args.method == "euler" else 0, delta_t=args.dt,
                         record_t=args.record, keep_lines=False, compute_stream=compute, on_pair=on_pair,
                         timing=timing if timed else None, segment_steps=args.segment if args.segment else -1,
-                        record_stride=n_pad)
+                        record_stride=n_pad, defer_lines=defer_lines)
         compute.synchronize(); comm.synchronize()
         return res
 
@@ -837,6 +843,9 @@ def main_chain(args, mesh, dev, world, rank):
                      + " during pair p (3 field buffers)") if chain.overlap_stream is not None else
                     "snapshot p+2 generated on a side stream beside pair p's launches, derived after pair p"
                     if args.config in (4, 5) else "none (every snapshot derived before the timed region)"),
+                "line_assembly": ("each pair's lines assembled on a side stream beside the next pair (second record "
+                                  "slab; the continuation points from mops_traj_last_points)" if defer_lines else
+                                  "each pair's lines assembled before the next pair starts"),
                 "record_gather": record_gather_text(world, args, per="pair", K=max(g // args.record for g in gaps),
                                                     collector=collector[0])},
             "nominal_particle_steps_per_call": n_all * n_steps,

@@ -281,6 +281,16 @@ mops_status mops_traj_finalize(int64_t n, int64_t K, const double* d_seeds, cons
                                double* d_velocity, double* d_temperature, double* d_salinity, double* d_last_point,
                                void* stream);
 
+/* mops_traj_finalize's d_last_point alone: each line's cleaned last point
+ * (RemoveNaNTrajectoriesAndReindex, src/Common/TrajectoryCommon.h:92-121:
+ * the last finite point before the first non-finite one) from the seeds and
+ * the records' positions, written at d_line[i] (NULL = identity).  What the
+ * next pair of a chain needs as its seeds (MOPSPathline.run's _last_pt,
+ * tutorial/pyMOPSAPI.py:1488), so the full line assembly can run
+ * beside the next pair.  Same values as mops_traj_finalize's bit for bit. */
+mops_status mops_traj_last_points(int64_t n, int64_t K, const double* d_seeds, const double* d_records,
+                                  int64_t record_stride, const int32_t* d_line, double* d_last_point, void* stream);
+
 /* RemoveNaNTrajectoriesAndReindex alone on n lines of P points each, in
  * place (device pointers; [n*P*3], [n*P*3], [n*P], [n*P], out [n*3]). */
 mops_status mops_remove_nan_lines(int64_t n, int64_t P, double* d_points, double* d_velocity,

@@ -20,7 +20,7 @@ EXPORTED = (
     "mops_field_destroy", "mops_field_bytes",
     "mops_locate_cells", "mops_locate_cells_hinted", "mops_order_particles", "mops_order_scratch_bytes",
     "mops_order_particles_live", "mops_permute_arrays", "mops_records_clear_dead",
-    "mops_traj_num_records", "mops_traj_num_steps", "mops_traj_advance", "mops_traj_finalize",
+    "mops_traj_num_records", "mops_traj_num_steps", "mops_traj_advance", "mops_traj_finalize", "mops_traj_last_points",
     "mops_remove_nan_lines", "mops_remove_nan_ragged", "mops_run_trajectories", "mops_build_id",
     # include/mops_io.h
     "mops_lines_geo", "mops_write_lines_vtp", "mops_write_lines_txt", "mops_write_pathline_binary",
@@ -140,6 +140,8 @@ def load(path: str | None = None):
     lib.mops_traj_advance.argtypes = [P, P, P, P, P, I64, I64, P, I64, P]; lib.mops_traj_advance.restype = st
     lib.mops_traj_finalize.argtypes = [I64, I64, P, P, I64, I32, P, P, P, P, P, P, P]
     lib.mops_traj_finalize.restype = st
+    lib.mops_traj_last_points.argtypes = [I64, I64, P, P, I64, P, P, P]
+    lib.mops_traj_last_points.restype = st
     lib.mops_remove_nan_lines.argtypes = [I64, I64, P, P, P, P, P, P]; lib.mops_remove_nan_lines.restype = st
     lib.mops_remove_nan_ragged.argtypes = [I64, P, P, P, P, P, P, P]; lib.mops_remove_nan_ragged.restype = st
     lib.mops_order_scratch_bytes.argtypes = [I64]; lib.mops_order_scratch_bytes.restype = I64

@@ -138,7 +138,7 @@ class PathlineChain:
     def run(self, seeds, depth: float, particle_depths=None, method: int = L.MOPS_EULER, delta_t: int = 60,
             record_t: int = 360, direction: int = L.MOPS_FORWARD, follow_last: bool = True, keep_lines: bool = True,
             compute_stream=None, on_pair=None, timing=None, segment_steps: int = -1, reorder: bool = True,
-            record_stride: int | None = None):
+            record_stride: int | None = None, defer_lines: bool = False):
         """Run all pairs; returns device tensors {points, velocity, temperature,
         salinity, lastPoint, death_step (of the last pair)} when ``keep_lines``,
         else only lastPoint/death_step.  ``on_pair(p, last, ps)`` is called after pair p
@@ -153,7 +153,11 @@ class PathlineChain:
         launches (long pairs: particles drift across many cells and a wave's lanes stop
         sharing stencils -- config 5's 30-day pairs run 9% faster re-sorted every 3 days).
         ``record_stride``: columns of the record slab (default n; a multi-GPU shard pads it to the
-        largest shard so every rank's slab gathers with one all-gather)."""
+        largest shard so every rank's slab gathers with one all-gather).  ``defer_lines``: each pair's lines
+        are assembled on a side stream beside the next pair, from a second record slab and side copies of
+        the seeds and slot ids; the next pair's seeds come from mops_traj_last_points (the same doubles as
+        the assembly's lastPoint).  ``on_pair`` then sees the set after the slab swap, so it must not read
+        ``ps.records`` (distributed.RecordGather does: keep it off there)."""
         import torch
         dev = self.device or torch.device("cuda", torch.cuda.current_device())
         cs = compute_stream or torch.cuda.current_stream(dev)
@@ -196,6 +200,8 @@ class PathlineChain:
         attempted = torch.zeros((), dtype=torch.int64, device=dev)
         ov = self.overlap_stream
         ready, pair_done = {}, {}
+        asm = torch.cuda.Stream(device=dev) if defer_lines else None
+        dl = dict(slab=None, seeds=None, ids=None, assembled=None)  # the deferred assembly's buffers
         for p in range(self.n_snapshots - 1):
             if overlap and p + 2 < self.n_snapshots:
                 # snapshot p+2 into the buffer pair p-1 released (pair 0: the third pooled buffer)
@@ -249,10 +255,33 @@ class PathlineChain:
                     if timing is not None:
                         e1.record(cs)
                         timing.append((e0, e1))
-                out = ps.finalize(pathline=True, stream=cs.cuda_stream)
+                if defer_lines:
+                    last = ps.last_points(stream=cs.cuda_stream)
+                    done_ev = torch.cuda.Event()
+                    done_ev.record(cs)
+                    asm.wait_event(done_ev)
+                    if dl["slab"] is None:
+                        dl.update(slab=torch.empty_like(ps.records), seeds=torch.empty_like(ps.seeds),
+                                  ids=torch.empty_like(ps.ids))
+                    if dl["assembled"] is not None:
+                        cs.wait_event(dl["assembled"])  # the spare slab's last reader is done before it is rewritten
+                    slab = ps.swap_records(dl["slab"])
+                    with torch.cuda.stream(asm):
+                        dl["seeds"].copy_(ps.seeds)
+                        dl["ids"].copy_(ps.ids)
+                    copied = torch.cuda.Event()
+                    copied.record(asm)
+                    cs.wait_event(copied)  # the next reseed rewrites seeds and ids in place
+                    with torch.cuda.stream(asm):
+                        out = ps.finalize_from(dl["seeds"], dl["ids"], slab, pathline=True, stream=asm.cuda_stream)
+                    dl["assembled"] = torch.cuda.Event()
+                    dl["assembled"].record(asm)
+                    dl["slab"] = slab
+                else:
+                    out = ps.finalize(pathline=True, stream=cs.cuda_stream)
+                    last = out["lastPoint"].clone()
                 dth = ps.death.to(torch.int64)
                 attempted += torch.where(dth < 0, torch.full_like(dth, cfg.n_steps), dth + 1).sum()
-                last = out["lastPoint"].clone()
                 if keep_lines:
                     sl = slice(None) if p == 0 else slice(1, None)
                     pts_acc.append(out["points"][:, sl]); vel_acc.append(out["velocity"][:, sl])
@@ -291,6 +320,8 @@ class PathlineChain:
                     self.make_field.release(f)  # kept for the next run (e.g. DeviceFieldRecycler)
                 else:
                     f.close()
+        if asm is not None:
+            cs.wait_stream(asm)  # the last pair's lines
         with torch.cuda.stream(cs):
             res = dict(lastPoint=last, death_step=ps.original(ps.death), attempted=attempted)
             if keep_lines:

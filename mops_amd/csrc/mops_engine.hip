@@ -2012,6 +2012,31 @@ __global__ void __launch_bounds__(256) assemble_clean_kernel(int64_t n, int K, c
     }
 }
 
+// The cleaned last point of every line alone -- assemble_clean_kernel's `last` (the last finite point
+// before the first non-finite one, the seed when the seed itself is not finite, else the final record;
+// RemoveNaNTrajectoriesAndReindex, TrajectoryCommon.h:92-121) -- without assembling the lines: a chained
+// pair's next seeds, so the full assembly can run beside the next pair (mops_traj_last_points).
+// One lane per slot; record k's x/y/z rows are read coalesced across the slots, stopping at the cut.
+__global__ void __launch_bounds__(256) last_point_kernel(int64_t n, int K, const double* __restrict__ seeds,
+                                                         const double* __restrict__ rec, int64_t stride,
+                                                         const int32_t* __restrict__ line, double* __restrict__ last) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    double lx = seeds[3 * i], ly = seeds[3 * i + 1], lz = seeds[3 * i + 2];
+    if (finite3(lx, ly, lz)) {
+        for (int k = 0; k < K; ++k) {
+            const double* r = rec + (int64_t)k * 6 * stride + i;
+            const double x = r[0], y = r[stride], z = r[2 * stride];
+            if (!finite3(x, y, z)) break;
+            lx = x; ly = y; lz = z;
+        }
+    }
+    const int64_t o = line ? (int64_t)line[i] : i;
+    last[3 * o] = lx;
+    last[3 * o + 1] = ly;
+    last[3 * o + 2] = lz;
+}
+
 // ===========================================================================
 // derived-field preprocessing (once per snapshot)
 // ===========================================================================
@@ -3805,6 +3830,17 @@ mops_status mops_traj_finalize(int64_t n, int64_t K, const double* d_seeds, cons
                                            d_sal);
         remove_nan_kernel<<<grid_for(n), kBlock, 0, s>>>(n, K + 1, nullptr, d_points, d_vel, d_tmp, d_sal, d_last);
     }
+    HIP_TRY(hipGetLastError());
+    return MOPS_OK;
+}
+
+mops_status mops_traj_last_points(int64_t n, int64_t K, const double* d_seeds, const double* d_records,
+                                  int64_t stride, const int32_t* d_line, double* d_last, void* stream) {
+    if (n < 0 || K <= 0 || K > INT32_MAX || !d_seeds || !d_records || !d_last || stride < n)
+        return fail(MOPS_ERR_INVALID, "mops_traj_last_points: invalid argument");
+    if (n == 0) return MOPS_OK;
+    last_point_kernel<<<(unsigned)((n + 255) / 256), 256, 0, (hipStream_t)stream>>>(n, (int)K, d_seeds, d_records,
+                                                                                   stride, d_line, d_last);
     HIP_TRY(hipGetLastError());
     return MOPS_OK;
 }

@@ -542,6 +542,34 @@ class ParticleSet:
             return int(self.cfg.recordT // self.cfg.deltaT)
         return int(self.cfg.recordT // math.gcd(int(self.cfg.recordT), int(self.cfg.deltaT)))
 
+    def last_points(self, stream=None):
+        """Each particle's cleaned last point in seed order (mops_traj_last_points): finalize's lastPoint
+        without the lines."""
+        torch = self.torch
+        last = torch.empty((self.n, 3), dtype=torch.float64, device=self.seeds.device)
+        L.check(L.load().mops_traj_last_points(self.n, self.K, C.c_void_p(self.seeds.data_ptr()),
+                                               C.c_void_p(self.records.data_ptr()), self.rec_stride,
+                                               C.c_void_p(self.ids.data_ptr()), C.c_void_p(last.data_ptr()),
+                                               _stream_handle(stream)), "mops_traj_last_points")
+        return last
+
+    def finalize_from(self, seeds, ids, records, pathline: bool, stream=None):
+        """finalize over another set's seeds, slot ids and record slab (a chain's deferred assembly: the
+        buffers of a finished pair while this set runs the next)."""
+        torch = self.torch
+        dev = self.seeds.device
+        P = self.K + 1
+        pts = torch.empty((self.n, P, 3), dtype=torch.float64, device=dev)
+        vel = torch.empty_like(pts)
+        tmp = torch.empty((self.n, P), dtype=torch.float64, device=dev)
+        sal = torch.empty_like(tmp)
+        L.check(L.load().mops_traj_finalize(self.n, self.K, C.c_void_p(seeds.data_ptr()), C.c_void_p(records.data_ptr()),
+                                            self.rec_stride, 1 if pathline else 0, C.c_void_p(ids.data_ptr()),
+                                            C.c_void_p(pts.data_ptr()), C.c_void_p(vel.data_ptr()),
+                                            C.c_void_p(tmp.data_ptr()), C.c_void_p(sal.data_ptr()), None,
+                                            _stream_handle(stream)), "mops_traj_finalize")
+        return dict(points=pts, velocity=vel, temperature=tmp, salinity=sal)
+
     def finalize(self, pathline: bool, stream=None, streams=None, timing=None):
         """Lines of every particle in seed order (mops_traj_finalize).  ``streams``: the
         advance_pipelined part streams -- each part's lines are assembled on its own stream right

@@ -188,3 +188,30 @@ def test_chain_resorts_after_deaths(engine_lib, oracle_lib, gpu, small_case):
     assert (np.linalg.norm(ref["points"], axis=-1) == 0).any(), "the case should leave dead particles' zero slots"
     for k in ("points", "velocity", "lastPoint"):
         assert np.array_equal(got[k].cpu().numpy(), ref[k]), k
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("euler", [True, False], ids=["euler", "rk4"])
+def test_chain_deferred_lines_match_oracle(engine_lib, oracle_lib, gpu, small_case, euler):
+    """PathlineChain(defer_lines=True): each pair's lines assembled on a side stream from a second record
+    slab while the next pair runs (its seeds from mops_traj_last_points), with re-sorts inside the pairs
+    (their record-slab swaps) and RK4 deaths: the lines, lastPoint and death steps equal the oracle chain's
+    and the serial assembly's bit for bit."""
+    from mops_amd import synth
+    from mops_amd.chain import PathlineChain, snapshot_field_factory
+    from mops_amd.engine import DeviceMesh
+    mesh, _, _ = small_case
+    snaps = [synth.make_snapshot(mesh, timestep=t, phase=0.35 * t) for t in range(4)]
+    seeds = synth.uniform_band_seeds(300, seed=23)
+    dm = DeviceMesh.from_mesh(mesh)
+    gaps = [43200, 21600, 32400]
+    chain = PathlineChain(dm, snapshot_field_factory(dm, lambda i: snaps[i]), len(snaps), gap_seconds=gaps)
+    kw = dict(depth=200.0, method=1 if euler else 0, delta_t=600, record_t=3600, segment_steps=5)
+    got = chain.run(seeds, defer_lines=True, **kw)
+    serial = chain.run(seeds, **kw)
+    ref = oracle_chain(oracle_lib, mesh, snaps, seeds, 200.0, None, gaps, 600, 3600, euler=euler)
+    for k in ("points", "velocity", "temperature", "salinity", "lastPoint"):
+        assert np.array_equal(got[k].cpu().numpy(), ref[k]), k
+    for k in ("points", "velocity", "temperature", "salinity", "lastPoint", "death_step"):
+        assert np.array_equal(got[k].cpu().numpy(), serial[k].cpu().numpy()), k
+
