@@ -233,13 +233,18 @@ def l1_block(key: str, unit_s: float):
     (TCP_TOTAL_CACHE_ACCESSES x 64 B, rocprofv3) over the unit's time, against the TD return peak."""
     e, src = measured_entry(key)
     acc = e.get("tcp_accesses_per_unit") if e else None
-    if acc is None:
+    if acc is None or e.get("td_busy") is None:
         return {"achieved": None, "peak": PEAK_L1_RETURN_GBS, "unit": "GB/s", "frac": None, "source": src}
-    ach = acc * 64.0 / unit_s / 1e9
-    return {"achieved": ach, "peak": PEAK_L1_RETURN_GBS, "peak_measured": L1_MEASURED_GBS, "unit": "GB/s",
-            "frac": ach / PEAK_L1_RETURN_GBS, "td_busy": e.get("td_busy"),
+    td = e["td_busy"]
+    tag = acc * 64.0 / unit_s / 1e9
+    # frac: the TD's measured busy fraction.  achieved: the return rate that busy fraction carries at the
+    # 64 B/clk/CU peak.  The tag-access rate (64 B per TCP access) is exact for coalesced 16-B lanes
+    # (tools/membench.hip mb_l1_x4) and an upper bound for scattered ones (config 4: above the peak).
+    return {"achieved": td * PEAK_L1_RETURN_GBS, "peak": PEAK_L1_RETURN_GBS, "peak_measured": L1_MEASURED_GBS,
+            "unit": "GB/s", "frac": td, "td_busy": td, "tag_rate_gbs": tag, "tag_rate_frac": tag / PEAK_L1_RETURN_GBS,
             "l1_to_l2_bytes_per_unit": (e.get("l1_to_l2_requests_per_unit") or 0.0) * 128.0,
-            "source": src + " TCP_TOTAL_CACHE_ACCESSES_sum x 64 B, TD_TD_BUSY_sum / 256 over GRBM_GUI_ACTIVE / 8"}
+            "source": src + " frac = TD_TD_BUSY_sum / 256 CUs over GRBM_GUI_ACTIVE / 8 XCDs; tag_rate = "
+                      "TCP_TOTAL_CACHE_ACCESSES_sum x 64 B over the launch time (upper bound for scattered lanes)"}
 
 
 def valu_block(key: str):
