@@ -175,7 +175,10 @@ class PathlineChain:
         # everything below is ordered on `cs` (the host never waits between pairs, so a
         # tensor touched on another stream could be read before `cs` has written it)
         with torch.cuda.stream(cs):
-            seeds0 = torch.as_tensor(np.ascontiguousarray(seeds, dtype=np.float64).reshape(-1, 3), device=dev)
+            if isinstance(seeds, torch.Tensor):  # (device-resident seeds: no upload; the set copies them)
+                seeds0 = seeds.to(device=dev, dtype=torch.float64).reshape(-1, 3).contiguous()
+            else:
+                seeds0 = torch.as_tensor(np.ascontiguousarray(seeds, dtype=np.float64).reshape(-1, 3), device=dev)
             n = int(seeds0.shape[0])
             per_particle = particle_depths is not None and len(particle_depths) == n
             pdep = (torch.as_tensor(np.asarray(particle_depths, dtype=np.float32), device=dev) if per_particle

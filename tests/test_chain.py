@@ -194,7 +194,8 @@ def test_chain_resorts_after_deaths(engine_lib, oracle_lib, gpu, small_case):
 @pytest.mark.parametrize("euler", [True, False], ids=["euler", "rk4"])
 def test_chain_deferred_lines_match_oracle(engine_lib, oracle_lib, gpu, small_case, euler):
     """PathlineChain(defer_lines=True): each pair's lines assembled on a side stream from a second record
-    slab while the next pair runs (its seeds from mops_traj_last_points), with re-sorts inside the pairs
+    slab while the next pair runs (its seeds from mops_traj_last_points; the first pair's seeds passed as a
+    device tensor), with re-sorts inside the pairs
     (their record-slab swaps) and RK4 deaths: the lines, lastPoint and death steps equal the oracle chain's
     and the serial assembly's bit for bit."""
     from mops_amd import synth
@@ -207,7 +208,8 @@ def test_chain_deferred_lines_match_oracle(engine_lib, oracle_lib, gpu, small_ca
     gaps = [43200, 21600, 32400]
     chain = PathlineChain(dm, snapshot_field_factory(dm, lambda i: snaps[i]), len(snaps), gap_seconds=gaps)
     kw = dict(depth=200.0, method=1 if euler else 0, delta_t=600, record_t=3600, segment_steps=5)
-    got = chain.run(seeds, defer_lines=True, **kw)
+    import torch
+    got = chain.run(torch.as_tensor(seeds, device="cuda"), defer_lines=True, **kw)  # (device-resident seeds too)
     serial = chain.run(seeds, **kw)
     ref = oracle_chain(oracle_lib, mesh, snaps, seeds, 200.0, None, gaps, 600, 3600, euler=euler)
     for k in ("points", "velocity", "temperature", "salinity", "lastPoint"):
