@@ -1,6 +1,6 @@
 """bench.py's roofline views from the committed PMC entries (profiles/pmc_traffic.json): every fraction is a
 measured busy fraction in [0, 1], and the limiter names the unit the counters show binding -- VALU issue for
-the cooperative config-3 kernel, the TD return for config 4.  Skipped when the entries were measured on another
+the cooperative config-3 kernel, the TD return for config 4, both together for config 2's streamline.  Skipped when the entries were measured on another
 engine build (bench.py then reports them as stale, never as this build's)."""
 import os
 import sys
@@ -12,6 +12,7 @@ sys.path.insert(0, ROOT)
 
 C3 = "ec30to60_chain3_euler_10000000_seg1440"
 C4 = "orrs18to6_chain4_euler_10000000_seg720"
+C2 = "ec30to60_streamline_euler_1000000_seg720_p2c6"
 
 
 def _entry(bench, key):
@@ -21,7 +22,8 @@ def _entry(bench, key):
     return e
 
 
-@pytest.mark.parametrize("key,launch_s,unit", [(C3, 0.530, "VALU issue"), (C4, 0.481, "texture-data return")])
+@pytest.mark.parametrize("key,launch_s,unit", [(C3, 0.530, "VALU issue"), (C4, 0.481, "texture-data return"),
+                                               (C2, 0.0247, "TD return and VALU issue")])
 def test_roofline_views_are_busy_fractions(key, launch_s, unit):
     import bench
     _entry(bench, key)
