@@ -216,10 +216,17 @@ def measured_traffic(key: str):
     return None, f"no PMC entry for {key}"
 
 
-def fp64_block(key: str, unit_s: float):
+def _entry_of(key_or_entry):
+    """(entry, provenance) for a workload key (this build's PMC entry only) or an entry given directly."""
+    if isinstance(key_or_entry, dict):
+        return key_or_entry, f"PMC entry {key_or_entry.get('workload')} (engine build {key_or_entry.get('engine_build')})"
+    return measured_entry(key_or_entry)
+
+
+def fp64_block(key, unit_s: float):
     """The FP64 vector-issue view of the same unit: PMC-counted FP64 add/mul/fma work over its time, against
     the FP64 vector peak (the path's arithmetic is FP64 scalar geometry; no MFMA applies)."""
-    e, src = measured_entry(key)
+    e, src = _entry_of(key)
     fl = e.get("fp64_flops_per_unit") if e else None
     if fl is None:
         return {"achieved": None, "peak": PEAK_FP64_TFLOPS, "unit": "TFLOP/s", "frac": None, "source": src}
@@ -228,10 +235,10 @@ def fp64_block(key: str, unit_s: float):
             "flops_per_unit": fl, "source": src + " SQ_INSTS_VALU_{ADD,MUL,FMA}_F64 x 64 lanes (fma = 2)"}
 
 
-def l1_block(key: str, unit_s: float):
+def l1_block(key, unit_s: float):
     """The memory-return view that binds the gather kernels: bytes the vector L1 returned to the lanes
     (TCP_TOTAL_CACHE_ACCESSES x 64 B, rocprofv3) over the unit's time, against the TD return peak."""
-    e, src = measured_entry(key)
+    e, src = _entry_of(key)
     acc = e.get("tcp_accesses_per_unit") if e else None
     if acc is None or e.get("td_busy") is None:
         return {"achieved": None, "peak": PEAK_L1_RETURN_GBS, "unit": "GB/s", "frac": None, "source": src}
@@ -247,17 +254,34 @@ def l1_block(key: str, unit_s: float):
                       "TCP_TOTAL_CACHE_ACCESSES_sum x 64 B over the launch time (upper bound for scattered lanes)"}
 
 
-def valu_block(key: str):
+def valu_block(key):
     """The VALU-issue view: how much of the SIMDs' cycles the kernel's vector instructions hold, from the same
     profile (tools/make_traffic.py valu_issue_model: FP64 add/mul/fma 4 SIMD-cycles per wave64, other VALU 2;
-    tools/merge_issue.py valu_busy: rocprof's VALUBusy from SQ_ACTIVE_INST_VALU)."""
-    e, src = measured_entry(key)
+    tools/merge_issue.py valu_busy: rocprof's VALUBusy from SQ_ACTIVE_INST_VALU).  As a roofline: achieved =
+    frac of the peak 1.0 (every SIMD issuing a VALU instruction every cycle)."""
+    e, src = _entry_of(key)
     if not e or e.get("valu_issue_model") is None:
         return {"frac": None, "source": src}
-    return {"frac": e["valu_issue_model"], "valu_busy": e.get("valu_busy"), "salu_busy": e.get("salu_busy"),
+    return {"achieved": e["valu_issue_model"], "peak": 1.0,
+            "frac": e["valu_issue_model"], "valu_busy": e.get("valu_busy"), "salu_busy": e.get("salu_busy"),
             "lds_busy": e.get("lds_busy"), "unit": "fraction of SIMD cycles",
             "source": src + " SQ_INSTS_VALU{,_ADD_F64,_MUL_F64,_FMA_F64}: (4 x FP64 + 2 x other) / (1024 SIMDs x "
                       "GRBM_GUI_ACTIVE / 8); valu_busy = SQ_ACTIVE_INST_VALU x 4 / 1024 / (GRBM_GUI_ACTIVE / 8)"}
+
+
+def limiter_kind(l1: dict, valu: dict) -> str:
+    """The roof that binds, from the counters (the rule limiter_text states): "l1_return" (TD >= 80% busy, or
+    clearly busier than the VALU), "valu_issue" (VALUBusy clearly above TD), else the busier of the two;
+    "hbm" when the PMC entry has neither view."""
+    td, vf = l1.get("td_busy"), valu.get("frac")
+    if td is None or vf is None:
+        return "hbm"
+    vb = valu.get("valu_busy") or vf
+    if td >= 0.8 or td > vb + 0.1:
+        return "l1_return"
+    if vb > td + 0.1:
+        return "valu_issue"
+    return "l1_return" if td >= vb else "valu_issue"
 
 
 def limiter_text(l1: dict, valu: dict) -> str:
@@ -285,18 +309,26 @@ def roofline_block(kernel: str, avg_kernel_s: float, psteps_per_launch: float, B
     traffic, src = measured_traffic(traffic_key)  # bytes per `per` unit
     achieved = traffic / avg_kernel_s / 1e9 if traffic is not None else None
     alg = B * psteps_per_launch / avg_kernel_s / 1e9
+    hbm = {"achieved": achieved, "peak": PEAK_HBM_GBS, "unit": "GB/s",
+           "frac": (achieved / PEAK_HBM_GBS) if achieved is not None else None, "traffic": traffic, "source": src}
+    l1, valu = l1_block(traffic_key, avg_kernel_s), valu_block(traffic_key)
+    kind = limiter_kind(l1, valu)
+    top = {"hbm": hbm, "l1_return": l1, "valu_issue": valu}[kind]
     return {
-        "bound": "hbm",
-        "achieved": achieved,
-        "peak": PEAK_HBM_GBS,
-        "unit": "GB/s",
-        "frac": (achieved / PEAK_HBM_GBS) if achieved is not None else None,
+        # the counter-chosen binding roof (limiter_kind); the HBM fraction BASELINE's metric asks for is the
+        # `hbm` view (the kernel is far below that roof: no workload here is DRAM-bound)
+        "bound": kind,
+        "achieved": top.get("achieved"),
+        "peak": top.get("peak"),
+        "unit": top.get("unit"),
+        "frac": top.get("frac"),
         "traffic": traffic,
         "traffic_source": src,
-        "limiter": limiter_text(l1_block(traffic_key, avg_kernel_s), valu_block(traffic_key)),
-        "valu_issue": valu_block(traffic_key),
+        "hbm": hbm,
+        "limiter": limiter_text(l1, valu),
+        "valu_issue": valu,
         "fp64_valu": fp64_block(traffic_key, avg_kernel_s),
-        "l1_return": l1_block(traffic_key, avg_kernel_s),
+        "l1_return": l1,
         "traffic_correction": ("bytes = 2 x FETCH_SIZE + WRITE_SIZE: the gfx950 factor 1/2 holds for this kernel's "
                                "scattered 80-B record reads too (tools/membench.hip: 4 GiB streamed -> FETCH_SIZE "
                                "0.500 of the bytes; 2^25 random 80-B records, one per 128-B line -> 2 x FETCH_SIZE "
@@ -756,13 +788,14 @@ def main_chain(args, mesh, dev, world, rank):
                 send[:n].copy_(last)
                 all_gather_flat(dist, gathered.view(-1), send.view(-1), args.backend)
 
+    on_pair.reads_records = gather_records  # (PathlineChain.run refuses defer_lines with a record-reading on_pair)
     seeds_dev = torch.as_tensor(np.ascontiguousarray(seeds, dtype=np.float64), device=dev)  # resident before timing
 
     def one_call(timed):
         res = chain.run(seeds_dev, depth=args.depth, method=1 if args.method == "euler" else 0, delta_t=args.dt,
                         record_t=args.record, keep_lines=False, compute_stream=compute, on_pair=on_pair,
                         timing=timing if timed else None, segment_steps=args.segment if args.segment else -1,
-                        record_stride=n_pad, defer_lines=defer_lines)
+                        record_stride=n_pad, defer_lines=defer_lines, compact_chunks=RK4_COMPACT_CHUNKS)
         compute.synchronize(); comm.synchronize()
         return res
 
@@ -808,9 +841,16 @@ def main_chain(args, mesh, dev, world, rank):
     kname = (f"traj_kernel<7,true,true,true|false> (pathline euler: the cooperative-tile instantiation where the "
              f"launch's sampled cells per wave are <= 6, else the plain one; both dispatched, the other exits at once)"
              if args.method == "euler" else "traj_kernel<7,true,false> (pathline rk4)")
+    key_tail = f"seg{seg_key}" if args.method == "euler" else f"compact{RK4_COMPACT_CHUNKS}"  # (RK4: compaction)
     roof = roofline_block(kname,
                           avg_kernel_s, psteps_per_launch, B,
-                          f"{mesh_class.lower()}_chain{args.config}_{args.method}_{args.particles}_seg{seg_key}")
+                          f"{mesh_class.lower()}_chain{args.config}_{args.method}_{args.particles}_{key_tail}")
+    # the north star's integrator (and the reference caller's default, MOPSPathline.run(method="rk4"),
+    # tutorial/pyMOPSAPI.py:1396) on the same chain, timed after the Euler line (N = 1; not part of value)
+    rk4 = None
+    if (world == 1 and args.method == "euler" and args.config == 3
+            and os.environ.get("MOPS_BENCH_NO_RK4") != "1"):
+        rk4 = chain_rk4_companion(args, chain, seeds_dev, compute, n, n_pad, gaps, B, mesh_class)
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         seed_cells = dmesh_locate_host(dmesh, seeds, dev)
@@ -834,7 +874,7 @@ def main_chain(args, mesh, dev, world, rank):
                        "sample of the 12)")
                     + ", snapshots generated + derived in HBM inside the timed region")
     if rank == 0:
-        print(json.dumps({
+        line = {
             "metric": "particle-steps/sec", "value": value, "unit": "particle-steps/s", "n_gpus": world,
             "steps": args.steps, "warmup": args.warmup, "ms_per_step": elapsed / args.steps * 1e3,
             "higher_is_better": True, "scaling": "strong" if args.config == 4 else "weak", "vs_baseline": None,
@@ -862,9 +902,63 @@ def main_chain(args, mesh, dev, world, rank):
             "attempted_particle_steps_per_call": attempted_all / args.steps,
             "roofline": roof,
             "cpu_baseline": cpu,
-        }))
+        }
+        if rk4 is not None:
+            line["rk4_companion"] = rk4
+        print(json.dumps(line))
     if world > 1:
         dist.destroy_process_group()
+
+
+RK4_COMPACT_CHUNKS = 6  # PathlineChain.run's default: launches per pair with a dead-particle compaction between
+
+
+def chain_rk4_companion(args, chain, seeds_dev, compute, n, n_pad, gaps, B, mesh_class):
+    """The same chain integrated with RK4 (MOPSPathline.run's default integrator): one untimed and one
+    timed chain, dead-particle compaction between RK4_COMPACT_CHUNKS launches per pair (quirk Q1 kills a
+    particle at its first cell crossing; a pair's dead particles restart the next pair at their lastPoint).
+    Reports attempted and nominal particle-steps, each pair's dead fraction and the RK4 kernel's roofline."""
+    import torch
+    timing4 = []
+    n_steps = sum(g // args.dt for g in gaps)
+
+    def run4(timed):
+        deads = []
+
+        def on4(p, last, ps):
+            with torch.cuda.stream(compute):
+                deads.append((ps.death >= 0).sum())
+        res = chain.run(seeds_dev, depth=args.depth, method=0, delta_t=args.dt, record_t=args.record,
+                        keep_lines=False, compute_stream=compute, on_pair=on4, timing=timing4 if timed else None,
+                        segment_steps=args.segment if args.segment else -1, record_stride=n_pad,
+                        compact=True, compact_chunks=RK4_COMPACT_CHUNKS)
+        compute.synchronize()
+        return res, deads
+
+    run4(False)
+    torch.cuda.synchronize()
+    t4 = time.perf_counter()
+    res4, deads = run4(True)
+    torch.cuda.synchronize()
+    el4 = time.perf_counter() - t4
+    att4 = float(res4["attempted"].item())
+    kms = [a.elapsed_time(b) for (a, b) in timing4]
+    avg_s = (sum(kms) / len(kms)) / 1e3
+    roof = roofline_block("traj_kernel<7,true,false,true|false> (pathline rk4: the cooperative-tile instantiation "
+                          "where the launch's sampled cells per wave are <= 6, else the plain one)",
+                          avg_s, att4 / len(kms), B,
+                          f"{mesh_class.lower()}_chain{args.config}_rk4_{args.particles}_compact{RK4_COMPACT_CHUNKS}")
+    roof["launches_per_chain"] = len(kms)
+    return {"value": att4 / el4, "unit": "particle-steps/s", "ms_per_chain": el4 * 1e3,
+            "attempted_particle_steps_per_chain": att4, "nominal_particle_steps_per_chain": float(n) * n_steps,
+            "dead_fraction_per_pair": [float(d.item()) / max(n, 1) for d in deads],
+            "dead_particle_compaction": f"{RK4_COMPACT_CHUNKS} launches per pair, live particles compacted between",
+            "kernel_ms_per_chain": sum(kms),
+            "roofline": roof,
+            "note": ("the same 7-pair chain integrated with RK4 (MOPSPathline.run's default, four evaluations per step "
+                     "in the step's start cell, quirk Q1: a particle dies at its first cell crossing and restarts "
+                     "the next pair at its lastPoint), one timed chain after the Euler line; value = attempted "
+                     "particle-steps / s; not part of the line's value")}
 
 
 def dmesh_locate_host(dmesh, seeds, dev):

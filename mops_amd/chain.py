@@ -138,7 +138,8 @@ class PathlineChain:
     def run(self, seeds, depth: float, particle_depths=None, method: int = L.MOPS_EULER, delta_t: int = 60,
             record_t: int = 360, direction: int = L.MOPS_FORWARD, follow_last: bool = True, keep_lines: bool = True,
             compute_stream=None, on_pair=None, timing=None, segment_steps: int = -1, reorder: bool = True,
-            record_stride: int | None = None, defer_lines: bool = False):
+            record_stride: int | None = None, defer_lines: bool = False, compact: bool | None = None,
+            compact_chunks: int = 6, on_lines=None, lines_chunk: int | None = None):
         """Run all pairs; returns device tensors {points, velocity, temperature,
         salinity, lastPoint, death_step (of the last pair)} when ``keep_lines``,
         else only lastPoint/death_step.  ``on_pair(p, last, ps)`` is called after pair p
@@ -156,9 +157,27 @@ class PathlineChain:
         largest shard so every rank's slab gathers with one all-gather).  ``defer_lines``: each pair's lines
         are assembled on a side stream beside the next pair, from a second record slab and side copies of
         the seeds and slot ids; the next pair's seeds come from mops_traj_last_points (the same doubles as
-        the assembly's lastPoint).  ``on_pair`` then sees the set after the slab swap, so it must not read
-        ``ps.records`` (distributed.RecordGather does: keep it off there)."""
+        the assembly's lastPoint).  ``on_pair`` then sees the set after the slab swap, so an ``on_pair``
+        that reads ``ps.records`` (an attribute ``reads_records`` = True, e.g. a distributed.RecordGather
+        collector) is refused with it.
+        ``compact``: dead-particle compaction (ParticleSet.compact) between ``compact_chunks`` launches per
+        pair -- live particles re-sorted to the front in locality order, the launch spread over them only;
+        None = on for RK4, whose stages must stay in the step's start cell (quirk Q1: a particle dies at its
+        first cell crossing, ~0.8 per particle-day at config 3).  Result-invariant.
+        ``on_lines(p, lines, ids)``: a writer hook instead of concatenating the lines in HBM (the reference
+        caller's lines_acc, pyMOPSAPI.py:1497-1518): each pair's lines are assembled in chunks of
+        ``lines_chunk`` particle slots (default all) and handed over as device tensors {points, velocity,
+        temperature, salinity} -- pairs after the first without their first sample, as the reference
+        appends them -- with ``ids`` (int32 device tensor: the particle of each row).  The chunk buffers
+        are reused: the hook consumes or copies them, on the current (compute) stream, before returning.
+        The next pair's seeds come from mops_traj_last_points.  Not with ``keep_lines`` or ``defer_lines``."""
         import torch
+        if on_lines is not None and (keep_lines or defer_lines):
+            raise ValueError("on_lines hands each pair's lines to the hook: not with keep_lines or defer_lines")
+        if defer_lines and on_pair is not None and getattr(on_pair, "reads_records", False):
+            raise ValueError("defer_lines swaps the record slab before on_pair: an on_pair that reads ps.records "
+                             "(reads_records) would see the next pair's slab")
+        do_compact = (int(method) == L.MOPS_RK4) if compact is None else bool(compact)
         dev = self.device or torch.device("cuda", torch.cuda.current_device())
         cs = compute_stream or torch.cuda.current_stream(dev)
         side = torch.cuda.Stream(device=dev)
@@ -223,9 +242,12 @@ class PathlineChain:
                 else:
                     s = last
                 if per_particle:
-                    if p > 0 and follow_last:
+                    if p > 0:
+                        # the reference updates the depths from every pair's last points, whether or not the
+                        # next seeds follow them (pyMOPSAPI.py:1490-1495; with follow_last the pre-run update
+                        # at :1465-1469 recomputes the same values from seeds = lastPoint).
                         # np.linalg.norm(axis=1) order: sqrt((x*x + y*y) + z*z)
-                        r = torch.sqrt((s[:, 0] * s[:, 0] + s[:, 1] * s[:, 1]) + s[:, 2] * s[:, 2])
+                        r = torch.sqrt((last[:, 0] * last[:, 0] + last[:, 1] * last[:, 1]) + last[:, 2] * last[:, 2])
                         pdep = torch.clamp(EARTH_RADIUS_M - r, min=0.0).to(torch.float32)
                     d = pdep
                 else:
@@ -246,15 +268,29 @@ class PathlineChain:
                     seg = max(1, REORDER_SECONDS // int(delta_t))
                 else:
                     seg = cfg.n_steps if segment_steps == 0 else int(segment_steps)  # records by absolute step
-                for s0 in range(0, cfg.n_steps, seg):
-                    if timing is not None:
-                        e0 = torch.cuda.Event(enable_timing=True); e1 = torch.cuda.Event(enable_timing=True)
-                        e0.record(cs)
-                    if reorder and s0 > 0:
+                bounds = set(range(0, cfg.n_steps, seg))
+                if do_compact:
+                    ch = max(1, int(compact_chunks))
+                    bounds |= {cfg.n_steps * k // ch for k in range(ch)}
+                bounds = sorted(bounds) + [cfg.n_steps]
+                live = None
+                for s0, s1 in zip(bounds[:-1], bounds[1:]):
+                    if s1 <= s0:
+                        continue
+                    if do_compact and s0 > 0:
+                        # live particles first (locality order), the dead after them; the launch covers the
+                        # live ones only.  Records written so far: slot 0's step-0 part .. the last completed
+                        # record (as ParticleSet.advance_pipelined)
+                        nrec = min(cfg.n_records, s0 // period + 1) if period else 1
+                        live = ps.compact(0, ps.n, cs, records_written=nrec)
+                    elif reorder and s0 > 0:
                         # every record slot moves with its particle: a particle that died earlier in the
                         # pair already holds the reference's zeros in its later slots
                         ps.reorder(stream=cs.cuda_stream)
-                    ps.advance(front, back, s0, min(s0 + seg, cfg.n_steps), stream=cs.cuda_stream)
+                    if timing is not None:  # (the launch alone: what rocprofv3 averages)
+                        e0 = torch.cuda.Event(enable_timing=True); e1 = torch.cuda.Event(enable_timing=True)
+                        e0.record(cs)
+                    ps.advance(front, back, s0, s1, stream=cs.cuda_stream, live_count=live)
                     if timing is not None:
                         e1.record(cs)
                         timing.append((e0, e1))
@@ -277,9 +313,17 @@ class PathlineChain:
                     cs.wait_event(copied)  # the next reseed rewrites seeds and ids in place
                     with torch.cuda.stream(asm):
                         out = ps.finalize_from(dl["seeds"], dl["ids"], slab, pathline=True, stream=asm.cuda_stream)
+                    if keep_lines:
+                        # allocated on `asm`, read on `cs` by the concatenation below (after cs.wait_stream(asm)):
+                        # the allocator must not hand the blocks back to `asm` while `cs` may still read them
+                        for t in out.values():
+                            t.record_stream(cs)
                     dl["assembled"] = torch.cuda.Event()
                     dl["assembled"].record(asm)
                     dl["slab"] = slab
+                elif on_lines is not None:
+                    last = ps.last_points(stream=cs.cuda_stream)
+                    self._hand_lines(ps, p, on_lines, lines_chunk, cs)
                 else:
                     out = ps.finalize(pathline=True, stream=cs.cuda_stream)
                     last = out["lastPoint"].clone()
@@ -333,6 +377,31 @@ class PathlineChain:
         if cs != torch.cuda.current_stream(dev):
             torch.cuda.current_stream(dev).wait_stream(cs)  # results are read on the caller's stream
         return res
+
+
+    @staticmethod
+    def _hand_lines(ps, p: int, on_lines, lines_chunk, cs):
+        """Pair p's lines to the writer hook, assembled in chunks of particle slots (run(on_lines=...))."""
+        import torch
+        n = ps.n
+        ch = n if not lines_chunk else max(1, min(int(lines_chunk), n))
+        P = ps.K + 1
+        dev = ps.seeds.device
+        bufs = getattr(ps, "_line_bufs", None)
+        if bufs is None or bufs["points"].shape[0] < ch or bufs["points"].shape[1] != P:
+            with torch.cuda.stream(cs):
+                bufs = dict(points=torch.empty((ch, P, 3), dtype=torch.float64, device=dev),
+                            velocity=torch.empty((ch, P, 3), dtype=torch.float64, device=dev),
+                            temperature=torch.empty((ch, P), dtype=torch.float64, device=dev),
+                            salinity=torch.empty((ch, P), dtype=torch.float64, device=dev))
+            ps._line_bufs = bufs
+        sl = slice(None) if p == 0 else slice(1, None)  # later pairs without their first sample (:1512-1516)
+        with torch.cuda.stream(cs):
+            for lo in range(0, n, ch):
+                hi = min(n, lo + ch)
+                out = {k: v[:hi - lo] for k, v in bufs.items()}
+                ps.finalize_range(lo, hi, out, pathline=True, stream=cs.cuda_stream)
+                on_lines(p, {k: v[:, sl] for k, v in out.items()}, ps.ids[lo:hi])
 
 
 def cu_split_streams(device, side_cus: int):

@@ -32,7 +32,9 @@
 #include <cstdio>
 #include <cstring>
 #include <limits>
+#include <mutex>
 #include <string>
+#include <utility>
 #include <vector>
 
 #include "mops_io.h"
@@ -104,6 +106,9 @@ inline int rec_ints_for(int maxv) { return ((1 + 2 * maxv) + 3) / 4 * 4; }
 #ifndef MOPS_COOP_PE
 #define MOPS_COOP_PE 1
 #endif
+#ifndef MOPS_COOP_PR
+#define MOPS_COOP_PR 1  // ... and pathline RK4
+#endif
 #ifndef MOPS_GR_COOP
 #define MOPS_GR_COOP 2  // level-pair records per LDS round trip in the tile instantiations (1: +1%, 3: +7%)
 #endif
@@ -162,6 +167,11 @@ struct mops_mesh {
     double4* d_exyz = nullptr;   // [E] edgeCoord
     double* d_rbf_coef = nullptr;  // [C][7][3] RBF coefficients (rbf_coef_kernel)
     int* d_rbf_slot = nullptr;     // [C][7] edge read by each slot, -1 = velocity 0
+    // the pathline launches' instantiation flag (coop_select_kernel), one per HIP stream: launches on
+    // one stream run in order, so the next launch's selection never overwrites a flag a running
+    // trajectory kernel still reads; allocated once per stream (no per-launch allocation)
+    mutable std::mutex coop_mu;
+    mutable std::vector<std::pair<hipStream_t, int*>> coop_flags;
 };
 
 struct mops_field {
@@ -206,6 +216,15 @@ struct mops_field {
 #endif
 
 namespace dev {
+
+// Hand-off of LDS data between the lanes of one wave (the cooperative tile's headers and pieces): the
+// wave's DS operations execute in issue order, so a wavefront-scope release/acquire pair -- no
+// instructions, only an ordering the compiler must keep -- around a code-motion barrier suffices
+__device__ __forceinline__ void wave_lds_sync() {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
 
 // Zeros of records [k0, K) of one particle (records [K][6][stride]): what the reference's
 // preallocated trajectory holds past a particle's death (the lambda returns, those points are
@@ -1203,14 +1222,22 @@ __device__ __forceinline__ void pair_sums(const Cell<MAXV>& c, const double* w, 
 // bottom" branch).  Otherwise bracket_mono walks from the hint inside the prefix,
 // and bracket_scan (the whole fixed-up column) runs when the walk would leave
 // it; the record of the final layer is then read.
-template <int MAXV, bool PATH, int GR, int NV, bool COOP = false>
+template <int MAXV, bool PATH, int GR, int NV, bool COOP = false, bool TCHK = false>
 __device__ __forceinline__ int layer_eval(const Cell<MAXV>& c, const double* w, int km, const Field& f, int L,
-                                          double d, int& hint, Pair& S, const double2* trec = nullptr) {
+                                          double d, int& hint, Pair& S, const double2* trec = nullptr,
+                                          int th = 0) {
     const double eps = 1e-8;
     const int h = hint;
     if (h >= 1 && h <= km) {  // km = -1: general bracket only (fast_ok)
-        // (a cooperative wave's tile holds every vertex's record at exactly this hinted layer)
-        pair_sums<MAXV, GR, NV, COOP>(c, w, f.pr, L, h, S, trec);
+        // (a cooperative wave's tile holds every vertex's record at the layer the lane's hint had when
+        // the tile was filled, th: always this one in Euler; an RK4 stage after another stage moved
+        // the hint (TCHK) gathers its records itself -- the next step regroups the wave)
+        if constexpr (COOP && TCHK) {
+            if (h == th) pair_sums<MAXV, GR, NV, true>(c, w, f.pr, L, h, S, trec);
+            else pair_sums<MAXV, GR, NV>(c, w, f.pr, L, h, S);
+        } else {
+            pair_sums<MAXV, GR, NV, COOP>(c, w, f.pr, L, h, S, trec);
+        }
         bool ok;
         if (h == 1 && d > S.zm + eps) {  // above the surface (z_0 = z_{h-1} here)
             ok = true;
@@ -1276,19 +1303,19 @@ __device__ __forceinline__ bool eval_stream(const Cell<MAXV>& c, int L, int V, c
 // pathline calc_velocity_at (MPASOVisualizerKernels.cpp:1124-1327).  The
 // attribute channel is not evaluated: FinalizeTrajectoryLinesWithAttrs never
 // reads it (TrajectoryCommon.h:176-185, quirk Q9), so it is unobservable.
-template <int MAXV, int GR, int NV, bool COOP = false>
+template <int MAXV, int GR, int NV, bool COOP = false, bool TCHK = false>
 __device__ __forceinline__ bool eval_path(const Cell<MAXV>& c, int L, int V, const Field& ff, const Field& fb,
                                           double px, double py, double pz, double d, double alpha, int& hint0,
                                           int& hint1, double& hx, double& hy, double& hz, double& wv,
-                                          const double2* tile = nullptr) {
+                                          const double2* tile = nullptr, int th0 = 0, int th1 = 0) {
     double w[MAXV];
     if (!weights<MAXV, NV, COOP>(c, L, V, px, py, pz, w, reinterpret_cast<const double4*>(tile))) return false;
     const bool wfin = weights_finite<MAXV, NV>(c, w);
     Pair F, B;
-    const int lf = layer_eval<MAXV, true, GR, MOPS_HEX_PAIRS_P ? NV : 0, COOP>(c, w, fast_ok<MAXV, NV>(c, c.mono0, wfin, w), ff, L, d, hint0, F,
-                                                                               tile + kTileOffRec);
-    const int lb = layer_eval<MAXV, true, GR, MOPS_HEX_PAIRS_P ? NV : 0, COOP>(c, w, fast_ok<MAXV, NV>(c, c.mono1, wfin, w), fb, L, d, hint1, B,
-                                                                               tile + kTileOffRec + kTileRec);
+    const int lf = layer_eval<MAXV, true, GR, MOPS_HEX_PAIRS_P ? NV : 0, COOP, TCHK>(
+        c, w, fast_ok<MAXV, NV>(c, c.mono0, wfin, w), ff, L, d, hint0, F, tile + kTileOffRec, th0);
+    const int lb = layer_eval<MAXV, true, GR, MOPS_HEX_PAIRS_P ? NV : 0, COOP, TCHK>(
+        c, w, fast_ok<MAXV, NV>(c, c.mono1, wfin, w), fb, L, d, hint1, B, tile + kTileOffRec + kTileRec, th1);
     if (lf < 0 || lb < 0) return false;
     const double xf = dmax(F.zk, dmin(d, F.zm));
     const double denf = F.zm - F.zk;
@@ -1314,17 +1341,17 @@ __device__ __forceinline__ bool eval_path(const Cell<MAXV>& c, int L, int V, con
 // One velocity evaluation.  A wave whose lanes all sit in hexagons (the bulk
 // of an MPAS mesh) runs the NV = 6 instantiation; any other wave the general
 // one.  Both compute the same operations in the same order.
-template <int MAXV, bool PATH, int GR>
+template <int MAXV, bool PATH, int GR, bool TCHK = false>
 __device__ __forceinline__ bool eval_at(bool hex, const Cell<MAXV>& c, int L, int V, const Field& f0,
                                         const Field& f1, double px, double py, double pz, double d, double alpha,
                                         int& hint0, int& hint1, double& hx, double& hy, double& hz, double& wv,
-                                        bool coop = false, const double2* tile = nullptr) {
+                                        bool coop = false, const double2* tile = nullptr, int th0 = 0, int th1 = 0) {
     if constexpr (MAXV == 7 && PATH) {
         if (coop) {  // wave-uniform: the tile instantiations
-            if (hex) return eval_path<MAXV, GR, 6, true>(c, L, V, f0, f1, px, py, pz, d, alpha, hint0, hint1, hx, hy,
-                                                         hz, wv, tile);
-            return eval_path<MAXV, GR, 0, true>(c, L, V, f0, f1, px, py, pz, d, alpha, hint0, hint1, hx, hy, hz, wv,
-                                                tile);
+            if (hex) return eval_path<MAXV, GR, 6, true, TCHK>(c, L, V, f0, f1, px, py, pz, d, alpha, hint0, hint1, hx,
+                                                               hy, hz, wv, tile, th0, th1);
+            return eval_path<MAXV, GR, 0, true, TCHK>(c, L, V, f0, f1, px, py, pz, d, alpha, hint0, hint1, hx, hy, hz,
+                                                      wv, tile, th0, th1);
         }
     }
     if constexpr (MAXV == 7) {
@@ -1485,9 +1512,14 @@ __global__ void __launch_bounds__(kTrajBlock, (TrajWaves<MAXV, PATH, EULER>::val
     c.V = a.V;
     // cooperative waves (see kTilePieces): the wave's LDS tile and its group headers; their kernel keeps no
     // per-lane normals (a tiled wave reads its cells' normals from the tile, any other wave computes them)
-    constexpr bool kCoop = COOP && PATH && EULER && MAXV == 7 && !RCache<MAXV, PATH, EULER>::value && MOPS_CPOLY &&
-                           MOPS_COOP_PE;
+    // (RK4 too: its four stages are evaluated in the step's start cell, quirk Q1, so a group's polygon and
+    // normals hold for the whole step; a stage whose hint left the tile's layer gathers its own records)
     constexpr bool kRC = RCache<MAXV, PATH, EULER>::value, kNrm = LdsNormals<MAXV, PATH, EULER>::value;
+    constexpr bool kCoop = COOP && PATH && MAXV == 7 && !kRC && kNrm && MOPS_CPOLY &&
+                           (EULER ? MOPS_COOP_PE : MOPS_COOP_PR);
+    // the tile and its headers are per block, and the group/header hand-offs between lanes rely on one
+    // wave's LDS operations running in order: one wave per block
+    static_assert(!kCoop || kTrajBlock == 64, "the cooperative tile needs one wave per block");
     // per-lane edge normals (Cell::nrm); in the cooperative kernel the same LDS holds either them (a wave in
     // lane-normal mode, c.lds_n) or the wave's tile
     constexpr int kNrmD = 3 * kNrmSlots(MAXV) * kTrajBlock, kTileD = 2 * MOPS_COOP_G * kTilePieces;
@@ -1671,7 +1703,7 @@ __global__ void __launch_bounds__(kTrajBlock, (TrajWaves<MAXV, PATH, EULER>::val
                         hd[3] = make_uint4(r1[0], r1[1], r1[2], r1[3]);
                         hd[4] = make_uint4(r1[4], r1[5], r1[6], r1[7]);
                     }
-                    __builtin_amdgcn_wave_barrier();  // (one wave per block: its LDS operations run in order)
+                    dev::wave_lds_sync();  // (one wave per block: its LDS operations run in order)
                     const int np = G * kTilePieces;
                     const uint32_t* hdi = reinterpret_cast<const uint32_t*>(s_hdr);
                     const double2* cpoly2 = reinterpret_cast<const double2*>(a.cpoly);
@@ -1699,14 +1731,14 @@ __global__ void __launch_bounds__(kTrajBlock, (TrajWaves<MAXV, PATH, EULER>::val
                             s_tile[i] = base[idx];
                         }
                     }
-                    __builtin_amdgcn_wave_barrier();
+                    dev::wave_lds_sync();
                     c.lds_n = false;  // (the tile overwrote the lane normals)
                 } else if (!c.lds_n) {  // tile mode -> lane-normal mode: each lane's normals of its cell
 #pragma unroll
                     for (int k = 0; k < 3 * kNrmSlots(MAXV); ++k)
                         c.nrm[k * kTrajBlock] = a.cnrm[(int64_t)cell * kCellNrm + k];
                     c.lds_n = true;
-                    __builtin_amdgcn_wave_barrier();
+                    dev::wave_lds_sync();
                 }
                 tcell = cell;
                 tkey = hk | (coop ? g : 0xff);
@@ -1737,18 +1769,25 @@ __global__ void __launch_bounds__(kTrajBlock, (TrajWaves<MAXV, PATH, EULER>::val
             double s1x, s1y, s1z, s1w, s2x, s2y, s2z, s2w, s3x, s3y, s3z, s3w, s4x, s4y, s4z, s4w;
             double qx, qy, qz;
             const double a1 = alpha;
-            bool ok = dev::eval_at<MAXV, PATH, PairGroup<PATH, EULER>::value>(hex, c, a.L, a.V, a.f0, a.f1, x, y, z, d, a1, hint0, hint1, s1x, s1y, s1z, s1w);
+            // the tile's layers per field (cooperative waves; see layer_eval)
+            const int th0 = (tkey >> 16) - 1, th1 = ((tkey >> 8) & 0xff) - 1;
+            constexpr int GR = PairGroup<PATH, EULER>::value;
+            bool ok = dev::eval_at<MAXV, PATH, GR, true>(hex, c, a.L, a.V, a.f0, a.f1, x, y, z, d, a1, hint0, hint1,
+                                                        s1x, s1y, s1z, s1w, coop, tile, th0, th1);
             if (!ok) { died = (int)step; break; }
             dev::advect((unsigned)step, x, y, z, s1x, s1y, s1z, dt * 0.5, qx, qy, qz);
             const double a2 = PATH ? dev::dclamp(a1 + 0.5 * a.dalpha, 0.0, 1.0) : 0.0;
-            ok = dev::eval_at<MAXV, PATH, PairGroup<PATH, EULER>::value>(hex, c, a.L, a.V, a.f0, a.f1, qx, qy, qz, d, a2, hint0, hint1, s2x, s2y, s2z, s2w);
+            ok = dev::eval_at<MAXV, PATH, GR, true>(hex, c, a.L, a.V, a.f0, a.f1, qx, qy, qz, d, a2, hint0, hint1, s2x,
+                                                   s2y, s2z, s2w, coop, tile, th0, th1);
             if (!ok) { died = (int)step; break; }
             dev::advect((unsigned)step, x, y, z, s2x, s2y, s2z, dt * 0.5, qx, qy, qz);
-            ok = dev::eval_at<MAXV, PATH, PairGroup<PATH, EULER>::value>(hex, c, a.L, a.V, a.f0, a.f1, qx, qy, qz, d, a2, hint0, hint1, s3x, s3y, s3z, s3w);
+            ok = dev::eval_at<MAXV, PATH, GR, true>(hex, c, a.L, a.V, a.f0, a.f1, qx, qy, qz, d, a2, hint0, hint1, s3x,
+                                                   s3y, s3z, s3w, coop, tile, th0, th1);
             if (!ok) { died = (int)step; break; }
             dev::advect((unsigned)step, x, y, z, s3x, s3y, s3z, dt, qx, qy, qz);
             const double a4 = PATH ? dev::dclamp(a1 + a.dalpha, 0.0, 1.0) : 0.0;
-            ok = dev::eval_at<MAXV, PATH, PairGroup<PATH, EULER>::value>(hex, c, a.L, a.V, a.f0, a.f1, qx, qy, qz, d, a4, hint0, hint1, s4x, s4y, s4z, s4w);
+            ok = dev::eval_at<MAXV, PATH, GR, true>(hex, c, a.L, a.V, a.f0, a.f1, qx, qy, qz, d, a4, hint0, hint1, s4x,
+                                                   s4y, s4z, s4w, coop, tile, th0, th1);
             if (!ok) { died = (int)step; break; }
             // (s1 + 2 s2 + 2 s3 + s4) / 6 -- cy::Vec3 operator order (:959-960)
             hx = (((s1x + s2x * 2.0) + s3x * 2.0) + s4x) / 6.0;
@@ -1861,10 +1900,13 @@ __device__ __forceinline__ bool finite3(double a, double b, double c) { return i
 // One thread per line.  Uniform lines (off == NULL): line i is points [i*P, (i+1)*P); ragged
 // lines: [off[i], off[i+1]) -- the reference's per-line vectors packed back to back.  An empty
 // line is left alone (the reference drops it, TrajectoryCommon.h:84-86: the host re-indexes).
+// Uniform lines written through a slot -> line map (line != NULL, a particle part's assembly into the
+// full outputs): thread i cleans line line[i], the one its slot's assembly wrote.
 __global__ void remove_nan_kernel(int64_t n, int64_t P, const int64_t* __restrict__ off, double* pts, double* vel,
-                                  double* tmp, double* sal, double* last) {
-    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+                                  double* tmp, double* sal, double* last, const int32_t* __restrict__ line = nullptr) {
+    int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n) return;
+    if (!off && line) i = line[i];
     const int64_t b = off ? off[i] : i * P;
     if (off) P = off[i + 1] - b;
     if (P <= 0) return;
@@ -2927,6 +2969,7 @@ void free_mesh(mops_mesh* m) {
     (void)hipFree(m->d_scratch);
     (void)hipFree(m->d_eoc); (void)hipFree(m->d_coe); (void)hipFree(m->d_exyz); (void)hipFree(m->d_rbf_coef);
     (void)hipFree(m->d_rbf_slot);
+    for (auto& f : m->coop_flags) (void)hipFree(f.second);
     delete m;
 }
 
@@ -2985,6 +3028,18 @@ __global__ void __launch_bounds__(256) coop_select_kernel(int64_t n, const int* 
     if (threadIdx.x == 0) *flag = (S > 0 && runs[0] <= (unsigned long long)MOPS_COOP_CELLS * (unsigned long long)S) ? 1 : 0;
 }
 
+// The stream's instantiation flag (mops_mesh::coop_flags), allocated on the stream's first pathline launch.
+static mops_status coop_flag(const mops_mesh* mesh, hipStream_t s, int** out) {
+    std::lock_guard<std::mutex> lk(mesh->coop_mu);
+    for (const auto& f : mesh->coop_flags)
+        if (f.first == s) { *out = f.second; return MOPS_OK; }
+    int* d = nullptr;
+    HIP_TRY(hipMalloc(reinterpret_cast<void**>(&d), sizeof(int)));
+    mesh->coop_flags.emplace_back(s, d);
+    *out = d;
+    return MOPS_OK;
+}
+
 template <int MAXV>
 void launch_traj(const TrajArgs& a, bool path, bool euler, hipStream_t s) {
     const unsigned g = (unsigned)((a.n + kTrajBlock - 1) / kTrajBlock);
@@ -2994,8 +3049,12 @@ void launch_traj(const TrajArgs& a, bool path, bool euler, hipStream_t s) {
                 if (a.coop_sel) traj_kernel<MAXV, true, true, true><<<g, kTrajBlock, 0, s>>>(a);
             }
             traj_kernel<MAXV, true, true><<<g, kTrajBlock, 0, s>>>(a);
+        } else {
+            if constexpr (MAXV == 7) {
+                if (a.coop_sel) traj_kernel<MAXV, true, false, true><<<g, kTrajBlock, 0, s>>>(a);
+            }
+            traj_kernel<MAXV, true, false><<<g, kTrajBlock, 0, s>>>(a);
         }
-        else traj_kernel<MAXV, true, false><<<g, kTrajBlock, 0, s>>>(a);
     } else {
         if (euler) traj_kernel<MAXV, false, true><<<g, kTrajBlock, 0, s>>>(a);
         else traj_kernel<MAXV, false, false><<<g, kTrajBlock, 0, s>>>(a);
@@ -3793,10 +3852,9 @@ mops_status mops_traj_advance(const mops_mesh* mesh, const mops_field* front, co
     const bool euler = (cfg->method == MOPS_EULER);
     hipStream_t s = (hipStream_t)stream;
     a.coop_sel = nullptr;
-    int* sel = nullptr;
-    if (MOPS_COOP_PE && back && euler && mesh->maxv == 7 && !p->d_order) {
-        // a per-launch flag (stream-ordered allocation: concurrent launches on other streams keep their own)
-        HIP_TRY(hipMallocAsync(reinterpret_cast<void**>(&sel), sizeof(int), s));
+    if ((euler ? MOPS_COOP_PE : MOPS_COOP_PR) && back && mesh->maxv == 7 && !p->d_order) {
+        int* sel = nullptr;
+        MOPS_TRY(coop_flag(mesh, s, &sel));
         coop_select_kernel<<<1, 256, 0, s>>>(p->n, p->d_cell, p->d_n_live, sel);
         a.coop_sel = sel;
     }
@@ -3809,7 +3867,6 @@ mops_status mops_traj_advance(const mops_mesh* mesh, const mops_field* front, co
         default: return fail(MOPS_ERR_UNSUPPORTED, "experiment build: MAXV 7 only");
 #endif
     }
-    if (sel) HIP_TRY(hipFreeAsync(sel, s));
     HIP_TRY(hipGetLastError());
     return MOPS_OK;
 }
@@ -3828,7 +3885,8 @@ mops_status mops_traj_finalize(int64_t n, int64_t K, const double* d_seeds, cons
     } else {
         assemble_kernel<<<nb, 256, 0, s>>>(n, K, d_seeds, d_records, stride, pathline, d_line, d_points, d_vel, d_tmp,
                                            d_sal);
-        remove_nan_kernel<<<grid_for(n), kBlock, 0, s>>>(n, K + 1, nullptr, d_points, d_vel, d_tmp, d_sal, d_last);
+        remove_nan_kernel<<<grid_for(n), kBlock, 0, s>>>(n, K + 1, nullptr, d_points, d_vel, d_tmp, d_sal, d_last,
+                                                         d_line);
     }
     HIP_TRY(hipGetLastError());
     return MOPS_OK;

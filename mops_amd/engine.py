@@ -397,6 +397,7 @@ class ParticleSet:
         L.check(lib.mops_records_clear_dead(n, C.c_void_p(self._n_live[key].data_ptr()), kw, self.K,
                                             C.c_void_p(self.records.data_ptr() + 8 * lo), self.rec_stride,
                                             _stream_handle(s)), "mops_records_clear_dead")
+        return self._n_live[key]
 
     def set_config(self, cfg: TrajectoryConfig):
         """Run the next call with ``cfg`` (a chained pair's own simulationDuration: its step and
@@ -452,8 +453,11 @@ class ParticleSet:
         return L.Particles(self.n, self.x.data_ptr(), self.y.data_ptr(), self.z.data_ptr(), self.depth.data_ptr(),
                            self.cell.data_ptr(), self.death.data_ptr(), None, None)  # physically ordered
 
-    def advance(self, front: DeviceField, back: DeviceField | None, step_begin: int, step_end: int, stream=None):
-        p = self.particles()
+    def advance(self, front: DeviceField, back: DeviceField | None, step_begin: int, step_end: int, stream=None,
+                live_count=None):
+        """Launch steps [step_begin, step_end) over every slot; ``live_count``: the device live count
+        compact(0, n) returned (only the leading live slots are spread over the XCDs)."""
+        p = self.particles() if live_count is None else self._sub_particles(0, self.n, live_count)
         st = L.load().mops_traj_advance(self.mesh.handle, front.handle, None if back is None else back.handle,
                                         C.byref(self._c), C.byref(p), int(step_begin), int(step_end),
                                         C.c_void_p(self.records.data_ptr()), self.rec_stride, _stream_handle(stream))
@@ -569,6 +573,22 @@ class ParticleSet:
                                             C.c_void_p(tmp.data_ptr()), C.c_void_p(sal.data_ptr()), None,
                                             _stream_handle(stream)), "mops_traj_finalize")
         return dict(points=pts, velocity=vel, temperature=tmp, salinity=sal)
+
+    def finalize_range(self, lo: int, hi: int, out: dict, pathline: bool, stream=None):
+        """The lines of slots [lo, hi) into ``out`` (device tensors points [m, P, 3], velocity [m, P, 3],
+        temperature / salinity [m, P], m = hi - lo) in slot order -- row i is particle ids[lo + i] -- a
+        bounded piece of finalize (PathlineChain's writer hook)."""
+        m = hi - lo
+        if m <= 0:
+            return out
+        L.check(L.load().mops_traj_finalize(m, self.K, C.c_void_p(self.seeds.data_ptr() + 24 * lo),
+                                            C.c_void_p(self.records.data_ptr() + 8 * lo), self.rec_stride,
+                                            1 if pathline else 0, None, C.c_void_p(out["points"].data_ptr()),
+                                            C.c_void_p(out["velocity"].data_ptr()),
+                                            C.c_void_p(out["temperature"].data_ptr()),
+                                            C.c_void_p(out["salinity"].data_ptr()), None, _stream_handle(stream)),
+                "mops_traj_finalize")
+        return out
 
     def finalize(self, pathline: bool, stream=None, streams=None, timing=None):
         """Lines of every particle in seed order (mops_traj_finalize).  ``streams``: the

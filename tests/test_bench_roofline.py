@@ -33,3 +33,42 @@ def test_roofline_views_are_busy_fractions(key, launch_s, unit):
     assert l1["achieved"] <= l1["peak"]
     assert 0.0 < valu["valu_busy"] <= 1.0
     assert bench.limiter_text(l1, valu).startswith(unit)
+
+
+def _entries_of_build(build):
+    import json
+    pm = json.load(open(os.path.join(ROOT, "profiles", "pmc_traffic.json")))
+    return {e["workload"]: e for e in pm if e.get("engine_build") == build}
+
+
+# the round-4 profiles (engine build 20548e0a, profiles/r04/c{2,3,4,5}): the counter-chosen roof of each
+R04 = "20548e0af4c5f230"
+
+
+@pytest.mark.parametrize("key,kind", [(C3, "valu_issue"), (C4, "l1_return"), (C2, "l1_return"),
+                                      ("orrs18to6_chain5_euler_12500000_seg4320", "valu_issue")])
+def test_roofline_bound_is_the_counter_chosen_limiter(key, kind, monkeypatch):
+    """The line's roofline.bound names the roof the counters show binding (bench.limiter_kind) -- VALU issue
+    for the cooperative configs 3/5 kernel, the TD return for config 4 (and config 2, where TD is the busier
+    of the two) -- and its achieved / peak / frac are that view's; the HBM fraction stays as the `hbm` view."""
+    import bench
+    ents = _entries_of_build(R04)
+    if key not in ents:
+        pytest.skip(f"no round-4 PMC entry {key}")
+    e = ents[key]
+    l1, valu = bench.l1_block(e, 0.5), bench.valu_block(e)
+    assert bench.limiter_kind(l1, valu) == kind
+    # roofline_block over the same entry (measured_entry / measured_traffic answer with it)
+    monkeypatch.setattr(bench, "measured_entry", lambda k: (e, "test"))
+    monkeypatch.setattr(bench, "measured_traffic", lambda k: (float(e["bytes_per_unit"]), "test"))
+    r = bench.roofline_block("k", 0.5, 1e10, 3660.0, key)
+    assert r["bound"] == kind
+    view = r[kind]
+    assert (r["achieved"], r["peak"], r["frac"]) == (view["achieved"], view["peak"], view["frac"])
+    assert 0.0 < r["frac"] <= 1.0
+    assert r["hbm"]["unit"] == "GB/s" and r["hbm"]["peak"] == bench.PEAK_HBM_GBS
+    assert r["hbm"]["frac"] == pytest.approx(e["bytes_per_unit"] / 0.5 / 1e9 / bench.PEAK_HBM_GBS)
+    if kind == "valu_issue":
+        assert r["limiter"].startswith("VALU issue")
+    else:
+        assert "TD" in r["limiter"]

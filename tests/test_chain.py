@@ -20,8 +20,10 @@ def oracle_chain(O, mesh, snaps, seeds, depth, particle_depths, gap, dt, rT, eul
     gaps = [gap] * (len(snaps) - 1) if np.isscalar(gap) else list(gap)
     for p in range(len(snaps) - 1):
         s = seeds if (p == 0 or not follow_last) else last
-        if pdep is not None and p > 0 and follow_last:
-            pdep = np.clip(EARTH_RADIUS_M - np.linalg.norm(s, axis=1), 0.0, None).astype(np.float32)
+        if pdep is not None and p > 0:
+            # per-particle depths follow the previous pair's last points whatever the seeds do
+            # (pyMOPSAPI.py:1490-1495; with follow_last, :1465-1469 recomputes the same from seeds = last)
+            pdep = np.clip(EARTH_RADIUS_M - np.linalg.norm(last, axis=1), 0.0, None).astype(np.float32)
         r = O.run(mesh, derived[p], derived[p + 1], s, depth=depth, depths=pdep, delta_t=dt, duration=gaps[p],
                   record_t=rT, euler=euler)
         sl = slice(None) if p == 0 else slice(1, None)
@@ -33,9 +35,11 @@ def oracle_chain(O, mesh, snaps, seeds, depth, particle_depths, gap, dt, rT, eul
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("method,per_particle", [(1, False), (0, False), (1, True)],
-                         ids=["euler", "rk4", "euler-perparticle"])
-def test_chain_matches_oracle(engine_lib, oracle_lib, gpu, small_case, method, per_particle):
+@pytest.mark.parametrize("method,per_particle,follow_last", [(1, False, True), (0, False, True), (1, True, True),
+                                                             (1, True, False), (0, True, False)],
+                         ids=["euler", "rk4", "euler-perparticle", "euler-perparticle-nofollow",
+                              "rk4-perparticle-nofollow"])
+def test_chain_matches_oracle(engine_lib, oracle_lib, gpu, small_case, method, per_particle, follow_last):
     from mops_amd import synth
     from mops_amd.chain import PathlineChain, snapshot_field_factory
     from mops_amd.engine import DeviceMesh
@@ -45,8 +49,10 @@ def test_chain_matches_oracle(engine_lib, oracle_lib, gpu, small_case, method, p
     pd = np.linspace(20.0, 600.0, len(seeds)).astype(np.float32) if per_particle else None
     dm = DeviceMesh.from_mesh(mesh)
     chain = PathlineChain(dm, snapshot_field_factory(dm, lambda i: snaps[i]), len(snaps), gap_seconds=21600)
-    got = chain.run(seeds, depth=300.0, particle_depths=pd, method=method, delta_t=600, record_t=3600)
-    ref = oracle_chain(oracle_lib, mesh, snaps, seeds, 300.0, pd, 21600, 600, 3600, euler=(method == 1))
+    got = chain.run(seeds, depth=300.0, particle_depths=pd, method=method, delta_t=600, record_t=3600,
+                    follow_last=follow_last)
+    ref = oracle_chain(oracle_lib, mesh, snaps, seeds, 300.0, pd, 21600, 600, 3600, euler=(method == 1),
+                       follow_last=follow_last)
     assert got["points"].shape[1] == 7 + 6          # 6 records + seed, then 6 more records
     for k in ("points", "velocity", "temperature", "salinity", "lastPoint"):
         assert np.array_equal(got[k].cpu().numpy(), ref[k]), k

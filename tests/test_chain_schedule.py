@@ -99,7 +99,7 @@ class _Shard:
         return old
 
 
-def _gather_worker(rank, world, port, q):
+def _gather_worker(rank, world, port, q, ring_records=1):
     import torch
     import torch.distributed as dist
     from oracle import oracle as O
@@ -142,23 +142,41 @@ def _gather_worker(rank, world, port, q):
             ok &= np.array_equal(got_seeds.numpy(), s_all)
             ok &= shard.records is not rec  # the particle set moved to the spare slab
             s_all = np.ascontiguousarray(ref["rec_pos"][:, K - 1])  # continuation points
-        # bounded ring: the last checkpoint again, gathered in chunks of one record through on_chunk
+        # bounded ring: the last checkpoint again, gathered in chunks of `ring_records` records through
+        # on_chunk (max_bytes below one checkpoint's gathered slab: the multi-chunk path config 5 takes)
         chunks = []
         shard2 = _Shard(rec.clone(), sd, ids, K)
-        ring = RecordGather(dist, shard2, world, backend="gloo", max_bytes=world * 6 * npad * 8,
+        ring = RecordGather(dist, shard2, world, backend="gloo", max_bytes=ring_records * world * 6 * npad * 8,
                             on_chunk=lambda g, k0, k1: chunks.append((k0, k1, g.clone())))
         ring.collect(shard2)
-        ok &= ring.chunk == 1 and [c[:2] for c in chunks] == [(0, 1), (1, 2)]
+        want = [(k0, min(K, k0 + ring_records)) for k0 in range(0, K, ring_records)]
+        ok &= ring.chunk == min(ring_records, kmax) and [c[:2] for c in chunks] == want
         whole = coll.gathered.view(-1)[: world * K * 6 * npad].view(world, K, 6, npad)
         ok &= torch.equal(torch.cat([c[2] for c in chunks], 1), whole)
+        # the first pair's 4 records through the same ring: a ragged last chunk when ring_records = 3
+        chunks.clear()
+        rec0 = torch.zeros((kmax, 6, npad), dtype=torch.float64)
+        rec0[:, :, : hi - lo] = torch.arange(kmax * 6 * (hi - lo), dtype=torch.float64).view(kmax, 6, -1) + 1e6 * rank
+        shard3 = _Shard(rec0, sd, ids, kmax)
+        ring.collect(shard3)
+        want = [(k0, min(kmax, k0 + ring.chunk)) for k0 in range(0, kmax, ring.chunk)]
+        ok &= [c[:2] for c in chunks] == want
+        g = torch.cat([c[2] for c in chunks], 1)  # [world, kmax, 6, npad]
+        for r in range(world):
+            rlo, rhi = shard_bounds(n_total, r, world)
+            exp = torch.arange(kmax * 6 * (rhi - rlo), dtype=torch.float64).view(kmax, 6, -1) + 1e6 * r
+            ok &= torch.equal(g[r, :, :, : rhi - rlo], exp) and bool((g[r, :, :, rhi - rlo:] == 0).all())
         q.put((rank, bool(ok)))
     finally:
         dist.destroy_process_group()
 
 
-def test_record_gather_gloo_world2_chain_shaped():
+@pytest.mark.parametrize("world,ring_records", [(2, 1), (3, 3), (4, 1), (4, 3)])
+def test_record_gather_gloo_chain_shaped(world, ring_records):
     """Two chained pairs with different record counts: each rank's slot-ordered records, gathered by
-    RecordGather and unsharded by the slot ids, equal the single-process (oracle) records bit for bit."""
+    RecordGather and unsharded by the slot ids, equal the single-process (oracle) records bit for bit.
+    91 particles: uneven, padded shards at 3 and 4 ranks (config 4's strong-scaling split of a
+    non-divisible N); the bounded ring in chunks of 1 or 3 records (3: a ragged last chunk)."""
     import multiprocessing as mp
     import socket
     from oracle import oracle as O
@@ -168,11 +186,11 @@ def test_record_gather_gloo_world2_chain_shaped():
         port = s.getsockname()[1]
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
-    procs = [ctx.Process(target=_gather_worker, args=(r, 2, port, q)) for r in range(2)]
+    procs = [ctx.Process(target=_gather_worker, args=(r, world, port, q, ring_records)) for r in range(world)]
     for p in procs:
         p.start()
     for p in procs:
         p.join(timeout=240)
     assert all(p.exitcode == 0 for p in procs)
-    res = dict(q.get(timeout=5) for _ in range(2))
-    assert res == {0: True, 1: True}
+    res = dict(q.get(timeout=5) for _ in range(world))
+    assert res == {r: True for r in range(world)}

@@ -153,6 +153,40 @@ def test_config3_full_size_pair(ec_case, oracle_lib):
     _check_shells(lines, death)
 
 
+def test_config3_full_size_pair_rk4(ec_case, oracle_lib):
+    """BASELINE config 3's pair with the north star's integrator (MOPSPathline.run's default, RK4): 1e7
+    particles at layer 10, dt 60 s, one daily pair through the chain driver as the bench runs it -- dead-
+    particle compaction between 6 launches, the cooperative-tile RK4 instantiation where waves share cells.
+    Quirk Q1 kills a particle at its first cell crossing, so this also runs the compaction and the dead-
+    particle records at full size; sampled lines (dead particles over-sampled) bit-exact against the oracle."""
+    import torch
+    import bench
+    from mops_amd.chain import PathlineChain
+    mesh, dm, f0, f1, r0, r1 = ec_case
+    depth = bench.layer_mid_depth(mesh, 10)
+    seeds = bench.make_seeds(10_000_000, 0)
+    chain = PathlineChain(dm, lambda i, stream: (f0, f1)[i], 2, gap_seconds=86400, own_fields=False)
+    got = chain.run(seeds, depth=depth, method=0, delta_t=60, record_t=3600, compact=True, compact_chunks=6)
+    torch.cuda.synchronize()
+    death = got["death_step"].cpu().numpy()
+    assert 0.2 < (death >= 0).mean() < 0.95  # Q1 deaths throughout the day (and survivors)
+    idx = _sample(len(seeds), death, k=256, k_dead=96, seed=4)
+    cells = _locate(dm, seeds[idx])
+    ref = oracle_lib.run(mesh, r0, r1, seeds[idx], depth=depth, delta_t=60, duration=86400, record_t=3600,
+                         euler=False, cells=cells)
+    _check_sample(got, death, idx, ref, pathline=True)
+    _check_shells(got, death)
+
+
+def _locate(dm, pts):
+    import torch
+    s = torch.as_tensor(np.ascontiguousarray(pts, dtype=np.float64), device="cuda")
+    c = torch.empty((s.shape[0],), dtype=torch.int32, device="cuda")
+    dm.locate(s.data_ptr(), c.data_ptr(), int(s.shape[0]))
+    torch.cuda.synchronize()
+    return c.cpu().numpy()
+
+
 def test_config3_full_size_chain(ec_case, oracle_lib):
     """Config-3 shape through the pair-chaining driver (3 daily snapshots = 2 pairs, 1e6 particles):
     continuation seeds, the exact hinted seed location between pairs and the line concatenation at
