@@ -111,6 +111,15 @@ int32_t mops_abi_version(void);
  * (6n doubles; zeros where |a| <= 1e-12). */
 mops_status mops_selftest_math(int64_t n, const double* d_x, double* d_out, int32_t op, void* stream);
 
+/* Self-test of the trajectory kernel's exact neighbour-table shortcut (not a
+ * reference entry point; maxEdges <= 7 meshes): for n points d_pts [n][3] in
+ * cells d_cells [n], d_out [n] gets bit 0 = the float bisector test kept the
+ * cell, bit 1 = the one-hop walk (MPASOVisualizerKernels.cpp:902-922) kept it,
+ * bits 8.. = the stay radius the test set (metres); -1 for an invalid cell.
+ * Bit 0 without bit 1 would be a wrong shortcut. */
+mops_status mops_selftest_walk(const mops_mesh* mesh, int64_t n, const double* d_pts, const int32_t* d_cells,
+                               int32_t* d_out, void* stream);
+
 /* ---- mesh / snapshots -------------------------------------------------- */
 
 /* Upload + re-layout a mesh.  Replaces MOPSApp::addGrid / MPASOGrid

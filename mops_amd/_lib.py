@@ -14,7 +14,7 @@ LIB_PATH = os.path.join(_HERE, "lib", "libmops_traj.so")
 
 # every symbol include/mops_traj.h declares (checked by tests/test_abi.py)
 EXPORTED = (
-    "mops_last_error", "mops_abi_version", "mops_selftest_math",
+    "mops_last_error", "mops_abi_version", "mops_selftest_math", "mops_selftest_walk",
     "mops_mesh_create", "mops_mesh_destroy", "mops_mesh_bytes", "mops_mesh_set_edges", "mops_cell_center_velocity_rbf",
     "mops_field_create", "mops_field_create_device", "mops_field_rebuild_device", "mops_field_create_derived", "mops_field_export", "mops_cell_to_vertex_attr",
     "mops_field_destroy", "mops_field_bytes",
@@ -106,6 +106,8 @@ def load(path: str | None = None):
     lib.mops_build_id.restype = C.c_char_p
     if hasattr(lib, "mops_selftest_math"):  # (older engine builds timed as variants lack the self-test)
         lib.mops_selftest_math.argtypes = [I64, P, P, I32, P]; lib.mops_selftest_math.restype = st
+    if hasattr(lib, "mops_selftest_walk"):
+        lib.mops_selftest_walk.argtypes = [P, I64, P, P, P, P]; lib.mops_selftest_walk.restype = st
     lib.mops_mesh_create.argtypes = [P, P, P]; lib.mops_mesh_create.restype = st
     lib.mops_mesh_destroy.argtypes = [P]; lib.mops_mesh_destroy.restype = None
     lib.mops_mesh_bytes.argtypes = [P]; lib.mops_mesh_bytes.restype = I64

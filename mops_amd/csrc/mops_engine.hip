@@ -70,10 +70,10 @@ constexpr int kBlock = 256;
 constexpr int kTrajBlock = MOPS_TRAJ_BLOCK;
 constexpr int kPairRec = 10;  // doubles per level-pair record (see mops_field::d_pr)
 #ifndef MOPS_PAIR_TEST
-#define MOPS_PAIR_TEST 1  // the walk's pair test (dev::walk)
+#define MOPS_PAIR_TEST 0  // the walk's pair test (dev::walk; superseded by dev::nbr_stay)
 #endif
 #ifndef MOPS_PAIR_TEST_P
-#define MOPS_PAIR_TEST_P 1  // ... in the pathline kernels
+#define MOPS_PAIR_TEST_P 0  // ... in the pathline kernels
 #endif
 // Compact per-lane LDS (traj_kernel): edge normals for polygon slots 0-5 only (slot 6, used by
 // heptagons alone, is computed in the evaluation: same operands, same bits) and the pair-test
@@ -125,6 +125,16 @@ constexpr int kTileRec = (kPairRec / 2) * 7;  // 7 level-pair records of one fie
 constexpr int kTileOffNrm = kTilePoly, kTileOffRec = kTilePoly + kTileNrm;
 constexpr int kTilePieces = kTilePoly + kTileNrm + 2 * kTileRec;  // 95 pieces = 1520 B per group
 constexpr int kTileHdr = 20;               // ints per group header: cell, nv, pad x2, front / back record index x 8
+// Neighbour table (maxEdges <= 7 meshes, mops_mesh::d_nbr): per cell 112 B = 7 x 16 B -- the centre as three
+// doubles, the 7 neighbour offsets q_k - c as floats, then the bitmask of the neighbours the walk considers.
+// dev::nbr_stay answers the walk's "does c stay?" from it, exactly, in 7 VMEM instead of the walk's ~20.
+#ifndef MOPS_NBR_TEST
+#define MOPS_NBR_TEST 1
+#endif
+#ifndef MOPS_NBR_RK4
+#define MOPS_NBR_RK4 0  // ... in the RK4 kernels too (measured: 6.64e9 vs 6.95e9 p-steps/s on the config-3 RK4 chain)
+#endif
+constexpr int kNbrQ = 7;                   // 16-B words per cell
 
 }  // namespace
 
@@ -153,6 +163,7 @@ struct mops_mesh {
     // slot j = {poly[j-1] (poly[-1] = poly[nv-1]), B_j = area(poly[j-1], poly[j], poly[j+1])}, zeros past nv
     double4* d_cpoly = nullptr;
     double* d_cnrm = nullptr;    // [C][kCellNrm] IsInMesh edge normals of the rotated polygon slots (maxv 7 meshes)
+    uint4* d_nbr = nullptr;      // [C][kNbrQ] neighbour table (cell_nbr_kernel, dev::nbr_stay; maxv 7 meshes)
     double* d_rloc2 = nullptr;       // [C] squared hinted-locate radius (locate_radius_kernel)
     double* d_ring = nullptr;        // [C] hinted-locate ring distance (locate_radius_kernel)
     // grow-only scratch for mops_order_particles (not re-entrant, like the reference's global app)
@@ -1088,6 +1099,57 @@ __device__ __forceinline__ int walk(Cell<MAXV>& c, int cell, double x, double y,
     return cell;
 }
 
+// Exact "c stays" test from the neighbour table (MOPS_NBR_TEST).  With e = p - c,
+// d_k = q_k - c and f_k = |d_k|^2 - 2 d_k.e = |p - q_k|^2 - |p - c|^2 (exactly, in real arithmetic), the
+// walk keeps c iff every considered neighbour's computed distance stays strictly above c's -- which holds
+// when f_k > 0 by more than the rounding of the reference's doubles.  Here f_k is evaluated in float from
+// the float offsets: g_k = fl(h_k - 2 fl(d_k.e)), h_k = fl(|d_k|^2), |g_k - f_k| < 2^-20 (h_k + |e|^2)
+// (float storage and arithmetic, 12.5 ulp-units at most), so g_k > M_k = 2^-17 (h_k + |e|^2) proves
+// f_k > 0.87 M_k, far above the doubles' rounding (2^-50 of the same scale).  Then every p' within
+// r = min_k (g_k - M_k) / (2 |d_k|) of p keeps the same margin (f_k moves by <= 2 |d_k| |p' - p|), so the
+// test also re-centres the stay ball on p with that radius.  Any other outcome (a bisector within the
+// margin, a crossing, a non-finite p) returns false and the caller walks as before.
+template <int MAXV, bool PT>
+__device__ __forceinline__ bool nbr_stay(Cell<MAXV>& c, int cell, double x, double y, double z,
+                                         const uint4* __restrict__ nbr) {
+    const uint4* t = nbr + (int64_t)cell * kNbrQ;
+    uint32_t w[4 * kNbrQ];
+#pragma unroll
+    for (int q = 0; q < kNbrQ; ++q) {
+        const uint4 v = t[q];
+        w[4 * q] = v.x; w[4 * q + 1] = v.y; w[4 * q + 2] = v.z; w[4 * q + 3] = v.w;
+    }
+    const double cx = __hiloint2double((int)w[1], (int)w[0]);
+    const double cy = __hiloint2double((int)w[3], (int)w[2]);
+    const double cz = __hiloint2double((int)w[5], (int)w[4]);
+    const float fx = (float)(x - cx), fy = (float)(y - cy), fz = (float)(z - cz);
+    const float e2 = fx * fx + fy * fy + fz * fz;
+    const uint32_t mask = w[27];
+    bool ok = true;
+    float r = __builtin_huge_valf();
+#pragma unroll
+    for (int k = 0; k < 7; ++k) {
+        if ((mask >> k) & 1u) {
+            const float dx = __uint_as_float(w[6 + 3 * k]), dy = __uint_as_float(w[7 + 3 * k]),
+                        dz = __uint_as_float(w[8 + 3 * k]);
+            const float h = dx * dx + dy * dy + dz * dz;
+            const float g = h - 2.0f * (dx * fx + dy * fy + dz * fz);
+            const float M = 0x1p-17f * (h + e2);
+            ok = ok & (g > M);  // (false for NaN / inf operands)
+            r = fminf(r, (g - M) * (0.5f * __builtin_amdgcn_rsqf(h)));
+        }
+    }
+    if (!ok) return false;
+    const double rr = (double)(r * (1.0f - 0x1p-16f));  // (rsq, the products: < 2^-20 relative)
+    c.cx = x; c.cy = y; c.cz = z;
+    c.rs2 = rr * rr * (1.0 - 1e-9);  // (inf when no neighbour is considered: the walk can only keep c)
+    if constexpr (PT) {  // the pair test's ball is centred on the walk's anchor, which just moved: drop it
+        if (MOPS_LDS_COMPACT) *c.rb2 = -1.0f;
+        else c.pr2[4 * kTrajBlock] = -1.0;
+    }
+    return true;
+}
+
 template <int MAXV, int NV>
 __device__ __forceinline__ bool weights_finite(const Cell<MAXV>& c, const double* w) {
     bool ok = true;
@@ -1380,6 +1442,7 @@ struct TrajArgs {
     const int* __restrict__ n_live;  // device count of leading live slots (compaction), NULL = all n
     const double4* __restrict__ cpoly;  // per-cell rotated polygon + Wachspress B_i (mops_mesh::d_cpoly)
     const double* __restrict__ cnrm;    // per-cell edge normals (mops_mesh::d_cnrm; NULL past maxEdges 7)
+    const uint4* __restrict__ nbr;      // per-cell neighbour table (mops_mesh::d_nbr; NULL past maxEdges 7)
     const int* __restrict__ coop_sel;   // per-launch device flag: 1 = the cooperative instantiation runs, 0 = the
                                         // plain one (the other exits at once); NULL = no selection
     double* px; double* py; double* pz;
@@ -1520,6 +1583,7 @@ __global__ void __launch_bounds__(kTrajBlock, (TrajWaves<MAXV, PATH, EULER>::val
     // the tile and its headers are per block, and the group/header hand-offs between lanes rely on one
     // wave's LDS operations running in order: one wave per block
     static_assert(!kCoop || kTrajBlock == 64, "the cooperative tile needs one wave per block");
+    constexpr bool kNbrT = MOPS_NBR_TEST && MAXV == 7 && (EULER || MOPS_NBR_RK4);  // dev::nbr_stay before a walk
     // per-lane edge normals (Cell::nrm); in the cooperative kernel the same LDS holds either them (a wave in
     // lane-normal mode, c.lds_n) or the wave's tile
     constexpr int kNrmD = 3 * kNrmSlots(MAXV) * kTrajBlock, kTileD = 2 * MOPS_COOP_G * kTilePieces;
@@ -1572,6 +1636,12 @@ __global__ void __launch_bounds__(kTrajBlock, (TrajWaves<MAXV, PATH, EULER>::val
                     stay_p = c.pr2[0] * x + c.pr2[kTrajBlock] * y + c.pr2[2 * kTrajBlock] * z +
                              c.pr2[3 * kTrajBlock] > 0.0;
             }
+            if constexpr (kNbrT) {
+                if (!stay_p && dev::nbr_stay<MAXV, kPairT>(c, cell, x, y, z, a.nbr)) {
+                    stay_p = true;
+                    atomicAdd(&dev::g_prof[13], 1ull);  // lane-steps the neighbour table kept in c
+                }
+            }
             const bool walking = !stay_p;
             bool loading = false;
             if (walking) {
@@ -1597,6 +1667,9 @@ __global__ void __launch_bounds__(kTrajBlock, (TrajWaves<MAXV, PATH, EULER>::val
                 if (!stay && e2 < (MOPS_LDS_COMPACT ? (double)*c.rb2 : c.pr2[4 * kTrajBlock]))  // second ball: only nb1 competes (dev::walk)
                     stay = c.pr2[0] * x + c.pr2[kTrajBlock] * y + c.pr2[2 * kTrajBlock] * z +
                            c.pr2[3 * kTrajBlock] > 0.0;
+            }
+            if constexpr (kNbrT) {
+                if (!stay) stay = dev::nbr_stay<MAXV, kPairT>(c, cell, x, y, z, a.nbr);  // exact: every bisector clear
             }
 #if defined(MOPS_ABL_NOWALK)  // ablation: never walk (wrong results; the walks' cost bound)
             if (false) {
@@ -1844,6 +1917,26 @@ __global__ void __launch_bounds__(kTrajBlock, (TrajWaves<MAXV, PATH, EULER>::val
     // slots never sampled: after a death, and past the last record step of a run whose
     // record period does not fill all K slots (streamline recordT % deltaT != 0)
     if (died >= 0 || a.step_end == a.n_steps) dev::clear_records(a.rec, a.rec_stride, pid, (rec_k == 0 && rec0) ? 1 : rec_k, a.K);
+}
+
+// the neighbour-table test against the walk it short-cuts (mops_selftest_walk): bit 0 = dev::nbr_stay kept
+// the cell, bit 1 = dev::walk kept it, bits 8.. = the stay-ball radius nbr_stay set, in metres (clamped)
+__global__ void selftest_walk_kernel(int64_t n, const double* __restrict__ pts, const int* __restrict__ cells,
+                                     const int* __restrict__ cellrec, const double4* __restrict__ cxyz,
+                                     const uint4* __restrict__ nbr, int C, int* __restrict__ out) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const int cell = cells[i];
+    if (cell < 0 || cell >= C) { out[i] = -1; return; }
+    const double x = pts[3 * i], y = pts[3 * i + 1], z = pts[3 * i + 2];
+    dev::Cell<7> c;
+    c.nv = cellrec[(int64_t)cell * (((1 + 2 * 7) + 3) / 4 * 4)];
+    c.rs2 = 0.0;
+    const bool a = dev::nbr_stay<7, false>(c, cell, x, y, z, nbr);
+    const double rad = a ? sqrt(c.rs2) : 0.0;
+    const bool b = dev::walk<7, false>(c, cell, x, y, z, cellrec, cxyz, C) == cell;
+    const int rq = (int)fmin(rad, 4.0e6);  // (< 2^22)
+    out[i] = (a ? 1 : 0) | (b ? 2 : 0) | (rq << 8);
 }
 
 // exact math helpers against the library (mops_selftest_math)
@@ -2608,6 +2701,37 @@ __global__ void mono_kernel(int64_t C, int maxv, int rec_ints, const int* cellre
     mono[i] = ok ? (0x80000000u | ((uint32_t)km << 20) | zmask) : 0u;
 }
 
+// The neighbour table of dev::nbr_stay (maxEdges <= 7): the centre c (doubles), the offsets q_k - c of
+// cellsOnCell slot k rounded to float (zero when not considered), and the mask of the slots the walk
+// considers (dev::walk's ok[k]: k < nEdges, a valid id).
+__global__ void cell_nbr_kernel(int64_t C, const int* __restrict__ cellrec, const double4* __restrict__ cxyz,
+                                uint4* __restrict__ nbr) {
+    const int64_t c = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (c >= C) return;
+    constexpr int MAXV = 7, REC = ((1 + 2 * MAXV) + 3) / 4 * 4;
+    const int* r = cellrec + c * REC;
+    const int nv = r[0];
+    const double4 q = cxyz[c];
+    uint32_t w[4 * kNbrQ];
+    w[0] = (uint32_t)__double2loint(q.x); w[1] = (uint32_t)__double2hiint(q.x);
+    w[2] = (uint32_t)__double2loint(q.y); w[3] = (uint32_t)__double2hiint(q.y);
+    w[4] = (uint32_t)__double2loint(q.z); w[5] = (uint32_t)__double2hiint(q.z);
+    uint32_t mask = 0;
+    for (int k = 0; k < MAXV; ++k) {
+        const int id = r[1 + MAXV + k];
+        const bool ok = k < nv && id >= 0 && id < C;
+        float d[3] = {0.0f, 0.0f, 0.0f};
+        if (ok) {
+            const double4 n = cxyz[id];
+            d[0] = (float)(n.x - q.x); d[1] = (float)(n.y - q.y); d[2] = (float)(n.z - q.z);
+            mask |= 1u << k;
+        }
+        for (int j = 0; j < 3; ++j) w[6 + 3 * k + j] = __float_as_uint(d[j]);
+    }
+    w[27] = mask;
+    for (int j = 0; j < kNbrQ; ++j) nbr[c * kNbrQ + j] = make_uint4(w[4 * j], w[4 * j + 1], w[4 * j + 2], w[4 * j + 3]);
+}
+
 // Each cell's polygon in the evaluation's rotated slot order (dev::Cell: slot j holds
 // poly[j-1], slot 0 poly[nv-1]) packed with its Wachspress numerator B_j = area(poly[j-1],
 // poly[j], poly[j+1]) -- the same device arithmetic as the in-kernel computation, so
@@ -2965,7 +3089,7 @@ void free_mesh(mops_mesh* m) {
     if (!m) return;
     (void)hipFree(m->d_cellrec); (void)hipFree(m->d_cxyz); (void)hipFree(m->d_vxyz); (void)hipFree(m->d_cov);
     (void)hipFree(m->d_bary);
-    (void)hipFree(m->d_bkeys); (void)hipFree(m->d_bcells); (void)hipFree(m->d_hkeys); (void)hipFree(m->d_hval); (void)hipFree(m->d_cell_rank); (void)hipFree(m->d_cpoly); (void)hipFree(m->d_cnrm); (void)hipFree(m->d_rloc2); (void)hipFree(m->d_ring);
+    (void)hipFree(m->d_bkeys); (void)hipFree(m->d_bcells); (void)hipFree(m->d_hkeys); (void)hipFree(m->d_hval); (void)hipFree(m->d_cell_rank); (void)hipFree(m->d_cpoly); (void)hipFree(m->d_cnrm); (void)hipFree(m->d_nbr); (void)hipFree(m->d_rloc2); (void)hipFree(m->d_ring);
     (void)hipFree(m->d_scratch);
     (void)hipFree(m->d_eoc); (void)hipFree(m->d_coe); (void)hipFree(m->d_exyz); (void)hipFree(m->d_rbf_coef);
     (void)hipFree(m->d_rbf_slot);
@@ -3129,6 +3253,19 @@ int mops_debug_stamps(unsigned long long* d_buf, long long cap, int* occ) {
 }
 #endif
 int32_t mops_abi_version(void) { return MOPS_ABI_VERSION; }
+
+mops_status mops_selftest_walk(const mops_mesh* mesh, int64_t n, const double* d_pts, const int32_t* d_cells,
+                               int32_t* d_out, void* stream) {
+    if (!mesh || n < 0 || (n > 0 && (!d_pts || !d_cells || !d_out)))
+        return fail(MOPS_ERR_INVALID, "mops_selftest_walk: invalid argument");
+    if (!mesh->d_nbr) return fail(MOPS_ERR_UNSUPPORTED, "mops_selftest_walk: no neighbour table (maxEdges > 7)");
+    if (n == 0) return MOPS_OK;
+    selftest_walk_kernel<<<grid_for(n), kBlock, 0, (hipStream_t)stream>>>(n, d_pts, d_cells, mesh->d_cellrec,
+                                                                         mesh->d_cxyz, mesh->d_nbr, (int)mesh->C,
+                                                                         d_out);
+    HIP_TRY(hipGetLastError());
+    return MOPS_OK;
+}
 
 mops_status mops_selftest_math(int64_t n, const double* d_x, double* d_out, int32_t op, void* stream) {
     if (n < 0 || (n > 0 && (!d_x || !d_out)) || (op != 0 && op != 1 && op != 2))
@@ -3316,6 +3453,8 @@ mops_status mops_mesh_create(const mops_mesh_desc* desc, void* stream, mops_mesh
                                                         m->d_rloc2, m->d_ring);
     if ((st = dmalloc(&m->d_cpoly, (size_t)(C * m->maxv), &acc)) != MOPS_OK) { free_mesh(m); return st; }
     if (m->maxv == 7 && (st = dmalloc(&m->d_cnrm, (size_t)(C * kCellNrm), &acc)) != MOPS_OK) { free_mesh(m); return st; }
+    if (m->maxv == 7 && (st = dmalloc(&m->d_nbr, (size_t)(C * kNbrQ), &acc)) != MOPS_OK) { free_mesh(m); return st; }
+    if (m->maxv == 7) cell_nbr_kernel<<<grid_for(C), kBlock, 0, s>>>(C, m->d_cellrec, m->d_cxyz, m->d_nbr);
     switch (m->maxv) {
         case 7: cell_poly_kernel<7><<<grid_for(C), kBlock, 0, s>>>(C, m->d_cellrec, m->d_vxyz, m->d_cpoly, m->d_cnrm); break;
         case 12: cell_poly_kernel<12><<<grid_for(C), kBlock, 0, s>>>(C, m->d_cellrec, m->d_vxyz, m->d_cpoly); break;
@@ -3835,6 +3974,7 @@ mops_status mops_traj_advance(const mops_mesh* mesh, const mops_field* front, co
     a.n_live = p->d_n_live;
     a.cpoly = mesh->d_cpoly;
     a.cnrm = mesh->d_cnrm;
+    a.nbr = mesh->d_nbr;
     a.px = p->d_x; a.py = p->d_y; a.pz = p->d_z; a.depth = p->d_depth; a.cell = p->d_cell; a.death = p->d_death_step;
     a.n = p->n;
     a.step_begin = step_begin; a.step_end = step_end; a.n_steps = n_steps;

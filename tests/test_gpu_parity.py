@@ -120,6 +120,64 @@ def test_fast_math_helpers_match_library(gpu, engine_lib):
     assert np.array_equal(o[:, :3].view(np.int64), o[:, 3:].view(np.int64)), "xdiv_norm3 != a / |a|"
 
 
+def _walk_selftest(engine_lib, dm, pts, cells):
+    import ctypes
+    import torch
+    d = torch.as_tensor(np.ascontiguousarray(pts, dtype=np.float64).reshape(-1), device="cuda")
+    c = torch.as_tensor(np.ascontiguousarray(cells, dtype=np.int32), device="cuda")
+    out = torch.empty((len(cells),), dtype=torch.int32, device="cuda")
+    assert engine_lib.mops_selftest_walk(dm.handle, len(cells), ctypes.c_void_p(d.data_ptr()),
+                                         ctypes.c_void_p(c.data_ptr()), ctypes.c_void_p(out.data_ptr()), None) == 0
+    torch.cuda.synchronize()
+    return out.cpu().numpy()
+
+
+def test_neighbour_table_shortcut_never_wrong(gpu, engine_lib, medium_case):
+    """dev::nbr_stay (the float bisector test that skips the one-hop walk, DESIGN.md section 4.11) may only
+    answer "c stays" where the walk keeps c: points placed on both sides of every cell's bisectors at
+    1e-6 m .. 1 km, at radii through the water column, plus non-finite points; and every point inside the
+    stay ball it sets (0.999 of its radius, random directions) keeps c under the walk too."""
+    from mops_amd.engine import DeviceMesh
+    mesh, _, _ = medium_case
+    dm = DeviceMesh.from_mesh(mesh)
+    rng = np.random.default_rng(77)
+    cc = np.asarray(mesh.cellCoord, dtype=np.float64).reshape(-1, 3)
+    coc = np.asarray(mesh.cellsOnCell, dtype=np.int64).reshape(mesh.nCells, -1)
+    ne = np.asarray(mesh.nEdgesOnCell, dtype=np.int64)
+    cells = rng.integers(0, mesh.nCells, 40000)
+    slot = (rng.integers(0, 7, len(cells)) % ne[cells])
+    nb = coc[cells, slot] - 1  # (1-based in the mesh arrays, 0 = none)
+    keep = (nb >= 0) & (nb < mesh.nCells)
+    cells, nb = cells[keep], nb[keep]
+    c, q = cc[cells], cc[nb]
+    d = q - c
+    n = d / np.linalg.norm(d, axis=1, keepdims=True)
+    t = np.cross(n, c / np.linalg.norm(c, axis=1, keepdims=True))
+    delta = np.sign(rng.uniform(-1, 1, len(cells))) * 10.0 ** rng.uniform(-6, 3, len(cells))
+    tau = rng.uniform(-0.3, 0.3, len(cells))[:, None] * np.linalg.norm(d, axis=1, keepdims=True)
+    p = 0.5 * (c + q) + delta[:, None] * n + tau * t
+    p *= ((6371000.0 - rng.uniform(0.0, 5000.0, len(cells))) / np.linalg.norm(p, axis=1))[:, None]
+    # cell centres, interior points and non-finite points too
+    p = np.concatenate([p, c[:500], c[:500] * 0.9999 + q[:500] * 0.0001,
+                        np.array([[np.nan, 0, 0], [np.inf, 1, 1], [0, 0, 0]])])
+    cells = np.concatenate([cells, cells[:500], cells[:500], np.array([0, 0, 0])])
+    out = _walk_selftest(engine_lib, dm, p, cells)
+    stay, walk_keeps = (out & 1) != 0, (out & 2) != 0
+    assert not np.any(stay & ~walk_keeps), "the neighbour test kept a cell the walk leaves"
+    inside = delta < -1.0  # clearly on c's side of this bisector
+    print(f"nbr_stay answered for {stay.mean():.3f} of the points, {stay[:len(delta)][inside].mean():.3f} of those "
+          f">1 m inside; the walk kept c for {walk_keeps.mean():.3f}")
+    assert stay[:len(delta)][inside].mean() > 0.5  # (it answers for most interior points)
+    # the stay ball: points at 0.999 of the radius in random directions keep c
+    r = (out >> 8).astype(np.float64)
+    sel = np.flatnonzero(stay & (r >= 1.0))[:20000]
+    u = rng.normal(size=(len(sel), 3))
+    u /= np.linalg.norm(u, axis=1, keepdims=True)
+    p2 = p[sel] + 0.999 * r[sel, None] * u
+    out2 = _walk_selftest(engine_lib, dm, p2, cells[sel])
+    assert np.all((out2 & 2) != 0), "a point inside the stay ball left the cell"
+
+
 def test_preprocessing_bitwise(dev_small, ref_small, small_case):
     mesh, s0, s1 = small_case
     _, f0, _ = dev_small
