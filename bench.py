@@ -636,6 +636,7 @@ def main():
                 "records": ps.K, "method": args.method, "parallelism": f"particle-shard x{world}",
                 "topography": args.topography,
                 "record_gather": record_gather_text(world, args, per="call", K=ps.K, collector=collector),
+                "record_gather_plan": collector.plan() if collector is not None else None,
             },
             "nominal_particle_steps_per_call": n_all * n_steps,
             "attempted_particle_steps_per_call": attempted_all,
@@ -897,7 +898,8 @@ def main_chain(args, mesh, dev, world, rank):
                                   "slab; the continuation points from mops_traj_last_points)" if defer_lines else
                                   "each pair's lines assembled before the next pair starts"),
                 "record_gather": record_gather_text(world, args, per="pair", K=max(g // args.record for g in gaps),
-                                                    collector=collector[0])},
+                                                    collector=collector[0]),
+                "record_gather_plan": collector[0].plan() if collector[0] is not None else None},
             "nominal_particle_steps_per_call": n_all * n_steps,
             "attempted_particle_steps_per_call": attempted_all / args.steps,
             "roofline": roof,

@@ -87,9 +87,30 @@ constexpr int kPairRec = 10;  // doubles per level-pair record (see mops_field::
 #define MOPS_NRM_SLOTS 5  // polygon slots whose normals live in LDS (MOPS_LDS_COMPACT; slots 5-6 computed per evaluation)
 #endif
 constexpr int kNrmSlots(int maxv) { return (MOPS_LDS_COMPACT && maxv > MOPS_NRM_SLOTS) ? MOPS_NRM_SLOTS : maxv; }
-#ifndef MOPS_PR_LEVEL_MAJOR
-#define MOPS_PR_LEVEL_MAJOR 1  // record (v, k) at index (k-1)*V + v (level-major; 0: v*(L-1) + k-1, vertex-major)
+// Level-pair record layout (mops_field::d_pr) in 16-B pieces: piece q (0..4) of the record of layer k1 = k-1
+// and vertex v.  MOPS_PR_PIECES = 1 (round 5): piece-major [L-1][5][V+1] -- piece q of consecutive vertices is
+// contiguous, and vertices are numbered in Morton order at mesh creation (MOPS_VPERM), so the lanes of one
+// gather instruction, which ask for piece q of the records of neighbouring cells' vertices, share 128-B lines:
+// the vector L1 / TD spends a cycle per distinct line of an instruction (tools/membench.hip mb_l1_scatter:
+// 8-16 lines 17 cycles, 32 lines 33, 64 lines 64).  The all-zero record is vertex V of every (layer, piece).
+// 0: record-major, level-major [L-1][V][5] (rounds 2-4) + one all-zero record after the last.
+#ifndef MOPS_PR_PIECES
+#define MOPS_PR_PIECES 0  // measured slower: record-major stays
 #endif
+#ifndef MOPS_VPERM
+#define MOPS_VPERM 1  // mesh vertices renumbered internally in the Morton order of their coordinates
+#endif
+// (all in 16-B piece units; uint32 throughout: mops_mesh_create checks pr_pieces < 2^32)
+__host__ __device__ __forceinline__ uint32_t pr_base(uint32_t k1, uint32_t v, uint32_t V) {  // piece 0
+    return MOPS_PR_PIECES ? k1 * 5u * (V + 1u) + v : (k1 * V + v) * 5u;
+}
+__host__ __device__ __forceinline__ uint32_t pr_qstride(uint32_t V) { return MOPS_PR_PIECES ? V + 1u : 1u; }
+__host__ __device__ __forceinline__ uint32_t pr_zero(uint32_t V, uint32_t L) {  // the all-zero record's piece 0
+    return MOPS_PR_PIECES ? V : (L - 1u) * V * 5u;
+}
+inline uint64_t pr_pieces(int64_t V, int L) {
+    return MOPS_PR_PIECES ? (uint64_t)(L - 1) * 5u * (uint64_t)(V + 1) : ((uint64_t)(L - 1) * (uint64_t)V + 1u) * 5u;
+}
 
 inline int rec_ints_for(int maxv) { return ((1 + 2 * maxv) + 3) / 4 * 4; }
 
@@ -130,6 +151,9 @@ constexpr int kTileHdr = 20;               // ints per group header: cell, nv, p
 // dev::nbr_stay answers the walk's "does c stay?" from it, exactly, in 7 VMEM instead of the walk's ~20.
 #ifndef MOPS_NBR_TEST
 #define MOPS_NBR_TEST 1
+#endif
+#ifndef MOPS_NBR_PAIR
+#define MOPS_NBR_PAIR 0  // dev::nbr_stay re-arms the pair test (with MOPS_PAIR_TEST / MOPS_PAIR_TEST_P)
 #endif
 #ifndef MOPS_NBR_RK4
 #define MOPS_NBR_RK4 0  // ... in the RK4 kernels too (measured: 6.64e9 vs 6.95e9 p-steps/s on the config-3 RK4 chain)
@@ -178,6 +202,12 @@ struct mops_mesh {
     double4* d_exyz = nullptr;   // [E] edgeCoord
     double* d_rbf_coef = nullptr;  // [C][7][3] RBF coefficients (rbf_coef_kernel)
     int* d_rbf_slot = nullptr;     // [C][7] edge read by each slot, -1 = velocity 0
+    // MOPS_VPERM: internal vertex i is the caller's vertex h_vold[i] (Morton order); every vertex-indexed array
+    // (coordinates, cellsOnVertex, the derived fields and records) is internal, and the vertex ids in the cell
+    // records are internal ids.  The vertex-array entry points map at the boundary (mops_field_create_derived,
+    // mops_field_export: host rows; mops_cell_to_vertex_attr: d_vold).  Empty / NULL = identity.
+    std::vector<int> h_vold;
+    int* d_vold = nullptr;
     // the pathline launches' instantiation flag (coop_select_kernel), one per HIP stream: launches on
     // one stream run in order, so the next launch's selection never overwrites a flag a running
     // trajectory kernel still reads; allocated once per stream (no per-launch allocation)
@@ -526,6 +556,9 @@ __device__ __forceinline__ double dclamp(double v, double lo, double hi) { retur
 #endif
 #ifndef MOPS_RC_PR
 #define MOPS_RC_PR 0
+#endif
+#ifndef MOPS_RC_PE_PLAIN
+#define MOPS_RC_PE_PLAIN 0
 #endif
 // modes without the register polygon: read a slot from the per-cell packed polygon (one 32-B
 // {x, y, z, B_j}, mops_mesh::d_cpoly) rather than the vertex array + B_j (1 = packed)
@@ -1127,6 +1160,7 @@ __device__ __forceinline__ bool nbr_stay(Cell<MAXV>& c, int cell, double x, doub
     const uint32_t mask = w[27];
     bool ok = true;
     float r = __builtin_huge_valf();
+    float r2 = __builtin_huge_valf(), n1x = 0.0f, n1y = 0.0f, n1z = 0.0f, h1 = 0.0f;  // MOPS_NBR_PAIR
 #pragma unroll
     for (int k = 0; k < 7; ++k) {
         if ((mask >> k) & 1u) {
@@ -1136,16 +1170,39 @@ __device__ __forceinline__ bool nbr_stay(Cell<MAXV>& c, int cell, double x, doub
             const float g = h - 2.0f * (dx * fx + dy * fy + dz * fz);
             const float M = 0x1p-17f * (h + e2);
             ok = ok & (g > M);  // (false for NaN / inf operands)
-            r = fminf(r, (g - M) * (0.5f * __builtin_amdgcn_rsqf(h)));
+            const float rk = (g - M) * (0.5f * __builtin_amdgcn_rsqf(h));
+            if constexpr (PT && MOPS_NBR_PAIR) {  // the nearest bisector and the second-nearest distance
+                const bool nearer = rk < r;
+                r2 = nearer ? r : fminf(r2, rk);
+                n1x = nearer ? dx : n1x; n1y = nearer ? dy : n1y; n1z = nearer ? dz : n1z; h1 = nearer ? h : h1;
+            }
+            r = fminf(r, rk);
         }
     }
     if (!ok) return false;
     const double rr = (double)(r * (1.0f - 0x1p-16f));  // (rsq, the products: < 2^-20 relative)
     c.cx = x; c.cy = y; c.cz = z;
     c.rs2 = rr * rr * (1.0 - 1e-9);  // (inf when no neighbour is considered: the walk can only keep c)
-    if constexpr (PT) {  // the pair test's ball is centred on the walk's anchor, which just moved: drop it
-        if (MOPS_LDS_COMPACT) *c.rb2 = -1.0f;
-        else c.pr2[4 * kTrajBlock] = -1.0;
+    if constexpr (PT) {
+        // The pair test's ball is centred on the anchor, which just moved.  MOPS_NBR_PAIR: re-arm it from the
+        // table -- inside the ball of the second-nearest bisector's radius r2 only the nearest one, k1, can be
+        // crossed, and f_k1(p') = h1 - 2 d1.(p' - c) = n.p' + k with n = -2 d1, k = h1 + 2 d1.c (DESIGN.md
+        // section 4.11; the float offsets' error over that ball is below M' / 32)
+        float rb2 = -1.0f;
+        if constexpr (MOPS_NBR_PAIR) {
+            if (r2 > r) {
+                const double rr2 = fmin((double)(r2 * (1.0f - 0x1p-16f)), sqrt((double)h1));
+                const double Mp = 0x1p-16 * ((double)h1 + 2.0 * (double)e2 * 1.01 + 2.0 * rr2 * rr2);
+                const double dx = n1x, dy = n1y, dz = n1z;
+                c.pr2[0 * kTrajBlock] = -2.0 * dx;
+                c.pr2[1 * kTrajBlock] = -2.0 * dy;
+                c.pr2[2 * kTrajBlock] = -2.0 * dz;
+                c.pr2[3 * kTrajBlock] = ((double)h1 + 2.0 * (dx * cx + dy * cy + dz * cz)) - Mp;
+                rb2 = __double2float_rz(rr2 * rr2 * (1.0 - 1e-9));
+            }
+        }
+        if (MOPS_LDS_COMPACT) *c.rb2 = rb2;
+        else c.pr2[4 * kTrajBlock] = rb2;
     }
     return true;
 }
@@ -1222,8 +1279,8 @@ __device__ __forceinline__ void pair_sums(const Cell<MAXV>& c, const double* w, 
     MOPS_MARK(300 + NV);
     S.zm = S.zk = S.wm = S.wk = 0.0;
     S.um0 = S.um1 = S.um2 = S.uk0 = S.uk1 = S.uk2 = 0.0;
-    // 32-bit record indices: V * L < 2^31 (mops_mesh_create), so v*(L-1) + k - 1 fits
-    const uint32_t zrec = (uint32_t)c.V * (uint32_t)(L - 1);
+    // 32-bit piece indices (mops_mesh_create: pr_pieces < 2^32)
+    const uint32_t zrec = pr_zero((uint32_t)c.V, (uint32_t)L), qs = pr_qstride((uint32_t)c.V);
     // tile reads (LDS latency) need fewer records in flight than gathers
     constexpr int GR_ = COOP ? MOPS_GR_COOP : GR;
 #pragma unroll
@@ -1234,22 +1291,18 @@ __device__ __forceinline__ void pair_sums(const Cell<MAXV>& c, const double* w, 
             for (int j = 0; j < GR_; ++j) {
                 const int v = v0 + j;
                 if (v >= MAXV) break;
-    #if defined(MOPS_ABL_PAIR1)
-            const uint32_t ri = (uint32_t)c.vid[0] * (uint32_t)(L - 1) + (uint32_t)(k - 1);
+#if defined(MOPS_ABL_PAIR1)
+            const uint32_t ri = pr_base((uint32_t)(k - 1), (uint32_t)c.vid[0], (uint32_t)c.V);
 #else
-#if MOPS_PR_LEVEL_MAJOR
-            const uint32_t ri = (v < nverts<NV>(c)) ? (uint32_t)(k - 1) * (uint32_t)c.V + (uint32_t)c.vid[v] : zrec;
-#else
-            const uint32_t ri = (v < nverts<NV>(c)) ? (uint32_t)c.vid[v] * (uint32_t)(L - 1) + (uint32_t)(k - 1) : zrec;
-#endif
+            const uint32_t ri = (v < nverts<NV>(c)) ? pr_base((uint32_t)(k - 1), (uint32_t)c.vid[v], (uint32_t)c.V) : zrec;
 #endif
                 if constexpr (COOP) {  // the wave's LDS tile: this vertex's record at the group's layer (zeros past nv)
 #pragma unroll
                     for (int q = 0; q < kPairRec / 2; ++q) a[j][q] = trec[(kPairRec / 2) * v + q];
                 } else {
-                    const double2* r = reinterpret_cast<const double2*>(pr + (uint64_t)ri * kPairRec);
+                    const double2* r = reinterpret_cast<const double2*>(pr);
 #pragma unroll
-                    for (int q = 0; q < kPairRec / 2; ++q) a[j][q] = r[q];
+                    for (int q = 0; q < kPairRec / 2; ++q) a[j][q] = r[ri + (uint32_t)q * qs];
                 }
             }
 #pragma unroll
@@ -1473,6 +1526,13 @@ struct TrajArgs {
 #ifndef MOPS_W_PR
 #define MOPS_W_PR 2  // pathline RK4
 #endif
+#ifndef MOPS_RK4_LOOP
+#define MOPS_RK4_LOOP 0  // 1: RK4 stages as a loop around one inlined evaluation (4x less code, but 220-240 spilled
+                         // VGPRs: pathline RK4 5.34e9 vs 6.97e9, streamline RK4 3.5e9 vs 6.9e9 p-steps/s, measured)
+#endif
+#ifndef MOPS_RK4_ACC
+#define MOPS_RK4_ACC 1  // RK4 stage velocities accumulated as they come (see traj_kernel)
+#endif
 #ifndef MOPS_GR_E
 #define MOPS_GR_E 1  // level-pair records in flight per round trip, Euler
 #endif
@@ -1516,14 +1576,18 @@ struct LdsNormals {
     static constexpr bool value =
         MAXV <= 7 && (EULER ? (PATH ? MOPS_NRM_PE : MOPS_NRM_SE) : (PATH ? MOPS_NRM_PR : MOPS_NRM_SR));
 };
-template <int MAXV, bool PATH, bool EULER>
+#ifndef MOPS_W_PE_PLAIN
+#define MOPS_W_PE_PLAIN MOPS_W_PE  // the plain (not cooperative) pathline Euler kernel
+#endif
+template <int MAXV, bool PATH, bool EULER, bool COOP = false>
 struct TrajWaves {
-    static constexpr int base = PATH ? (EULER ? MOPS_W_PE : MOPS_W_PR) : (EULER ? MOPS_W_SE : MOPS_W_SR);
+    static constexpr int base = PATH ? (EULER ? (COOP ? MOPS_W_PE : MOPS_W_PE_PLAIN) : MOPS_W_PR)
+                                     : (EULER ? MOPS_W_SE : MOPS_W_SR);
     static constexpr int value = MAXV <= 7 ? base : (EULER ? 2 : 1);
 };
 
 template <int MAXV, bool PATH, bool EULER, bool COOP = false>
-__global__ void __launch_bounds__(kTrajBlock, (TrajWaves<MAXV, PATH, EULER>::value)) traj_kernel(TrajArgs a) {
+__global__ void __launch_bounds__(kTrajBlock, (TrajWaves<MAXV, PATH, EULER, COOP>::value)) traj_kernel(TrajArgs a) {
     if (a.coop_sel && ((*a.coop_sel != 0) != COOP)) return;  // the other instantiation runs this launch
     // XCD-aware mapping: blocks b, b+8, ... share an XCD (L2); give each XCD a
     // contiguous range of the locality-ordered particles (bijective remap)
@@ -1577,7 +1641,10 @@ __global__ void __launch_bounds__(kTrajBlock, (TrajWaves<MAXV, PATH, EULER>::val
     // per-lane normals (a tiled wave reads its cells' normals from the tile, any other wave computes them)
     // (RK4 too: its four stages are evaluated in the step's start cell, quirk Q1, so a group's polygon and
     // normals hold for the whole step; a stage whose hint left the tile's layer gathers its own records)
-    constexpr bool kRC = RCache<MAXV, PATH, EULER>::value, kNrm = LdsNormals<MAXV, PATH, EULER>::value;
+    // (MOPS_RC_PE_PLAIN: the plain -- not cooperative -- pathline Euler kernel, which runs the sparse waves of
+    // config 4, keeps the polygon in registers: 12 fewer VMEM per evaluation for a TD-bound launch)
+    constexpr bool kRC = RCache<MAXV, PATH, EULER>::value || (MOPS_RC_PE_PLAIN && PATH && EULER && !COOP && MAXV <= 7),
+                   kNrm = LdsNormals<MAXV, PATH, EULER>::value;
     constexpr bool kCoop = COOP && PATH && MAXV == 7 && !kRC && kNrm && MOPS_CPOLY &&
                            (EULER ? MOPS_COOP_PE : MOPS_COOP_PR);
     // the tile and its headers are per block, and the group/header hand-offs between lanes rely on one
@@ -1755,19 +1822,14 @@ __global__ void __launch_bounds__(kTrajBlock, (TrajWaves<MAXV, PATH, EULER>::val
     #endif
                 if (coop) {
                     if (lead) {  // the group's header: {cell, nv}, then each slot's level-pair record index per field
-                        const uint32_t zr = (uint32_t)a.V * (uint32_t)(a.L - 1);
+                        const uint32_t zr = pr_zero((uint32_t)a.V, (uint32_t)a.L);
                         uint32_t r0[8], r1[8];
     #pragma unroll
                         for (int v = 0; v < 8; ++v) {
                             const bool on = v < c.nv && v < MAXV;
                             const uint32_t vid = (uint32_t)c.vid[v < MAXV ? v : 0];
-    #if MOPS_PR_LEVEL_MAJOR
-                            r0[v] = (on && hint0 >= 1 && hint0 <= a.L - 1) ? (uint32_t)(hint0 - 1) * (uint32_t)a.V + vid : zr;
-                            r1[v] = (on && hint1 >= 1 && hint1 <= a.L - 1) ? (uint32_t)(hint1 - 1) * (uint32_t)a.V + vid : zr;
-    #else
-                            r0[v] = (on && hint0 >= 1 && hint0 <= a.L - 1) ? vid * (uint32_t)(a.L - 1) + (uint32_t)(hint0 - 1) : zr;
-                            r1[v] = (on && hint1 >= 1 && hint1 <= a.L - 1) ? vid * (uint32_t)(a.L - 1) + (uint32_t)(hint1 - 1) : zr;
-    #endif
+                            r0[v] = (on && hint0 >= 1 && hint0 <= a.L - 1) ? pr_base((uint32_t)(hint0 - 1), vid, (uint32_t)a.V) : zr;
+                            r1[v] = (on && hint1 >= 1 && hint1 <= a.L - 1) ? pr_base((uint32_t)(hint1 - 1), vid, (uint32_t)a.V) : zr;
                         }
                         uint4* hd = reinterpret_cast<uint4*>(s_hdr + g * (kTileHdr / 4));
                         hd[0] = make_uint4((uint32_t)cell, (uint32_t)c.nv, 0u, 0u);
@@ -1800,7 +1862,7 @@ __global__ void __launch_bounds__(kTrajBlock, (TrajWaves<MAXV, PATH, EULER>::val
                             const double2* base = isp ? cpoly2 : (isn ? cnrm2 : (f1 ? pr1 : pr0));
                             const uint64_t idx = isp ? ((uint64_t)cl * MAXV + (uint32_t)(pc >> 1)) * 2 + (uint32_t)(pc & 1)
                                                      : (isn ? (uint64_t)cl * kTileNrm + (uint32_t)(pc - kTileOffNrm)
-                                                            : (uint64_t)ri * (kPairRec / 2) + (uint32_t)q);
+                                                            : (uint64_t)(ri + (uint32_t)q * pr_qstride((uint32_t)a.V)));
                             s_tile[i] = base[idx];
                         }
                     }
@@ -1839,12 +1901,64 @@ __global__ void __launch_bounds__(kTrajBlock, (TrajWaves<MAXV, PATH, EULER>::val
             dev::rotate((unsigned)step, x, y, z, ax, ay, az, th, nx, ny, nz);
         } else {
             const double dt = (double)a.delta_t;
-            double s1x, s1y, s1z, s1w, s2x, s2y, s2z, s2w, s3x, s3y, s3z, s3w, s4x, s4y, s4z, s4w;
-            double qx, qy, qz;
             const double a1 = alpha;
             // the tile's layers per field (cooperative waves; see layer_eval)
             const int th0 = (tkey >> 16) - 1, th1 = ((tkey >> 8) & 0xff) - 1;
             constexpr int GR = PairGroup<PATH, EULER>::value;
+#if MOPS_RK4_LOOP
+            // The four stages as one loop around a single inlined evaluation (the unrolled form inlines
+            // four copies of every eval_path instantiation: ~90k instructions in the cooperative RK4
+            // kernel).  The sums keep the reference's association, ((s1 + 2 s2) + 2 s3) + s4 (:959-960).
+            const double a2 = PATH ? dev::dclamp(a1 + 0.5 * a.dalpha, 0.0, 1.0) : 0.0;
+            const double a4 = PATH ? dev::dclamp(a1 + a.dalpha, 0.0, 1.0) : 0.0;
+            double qx = x, qy = y, qz = z;
+            bool ok = true;
+#pragma nounroll
+            for (int stg = 0; stg < 4; ++stg) {
+                double sx, sy, sz, sw;
+                const double as = stg == 0 ? a1 : (stg == 3 ? a4 : a2);
+                ok = dev::eval_at<MAXV, PATH, GR, true>(hex, c, a.L, a.V, a.f0, a.f1, qx, qy, qz, d, as, hint0, hint1,
+                                                        sx, sy, sz, sw, coop, tile, th0, th1);
+                if (!ok) break;
+                if (stg == 0) {
+                    hx = sx; hy = sy; hz = sz; wv = sw;
+                } else if (stg == 3) {
+                    hx = hx + sx; hy = hy + sy; hz = hz + sz; wv = wv + sw;
+                } else {
+                    hx = hx + sx * 2.0; hy = hy + sy * 2.0; hz = hz + sz * 2.0; wv = wv + 2.0 * sw;
+                }
+                if (stg < 3) dev::advect((unsigned)step, x, y, z, sx, sy, sz, stg == 2 ? dt : dt * 0.5, qx, qy, qz);
+            }
+            if (!ok) { died = (int)step; break; }
+            hx = hx / 6.0; hy = hy / 6.0; hz = hz / 6.0; wv = wv / 6.0;
+#elif MOPS_RK4_ACC
+            // The stage velocities summed as they come, in the reference's association ((s1 + 2 s2) + 2 s3) + s4
+            // (:959-960): the same operations as the sum at the end, without s1..s3 live across the stages
+            double sx, sy, sz, sw, qx, qy, qz;
+            bool ok = dev::eval_at<MAXV, PATH, GR, true>(hex, c, a.L, a.V, a.f0, a.f1, x, y, z, d, a1, hint0, hint1,
+                                                        sx, sy, sz, sw, coop, tile, th0, th1);
+            if (!ok) { died = (int)step; break; }
+            hx = sx; hy = sy; hz = sz; wv = sw;
+            dev::advect((unsigned)step, x, y, z, sx, sy, sz, dt * 0.5, qx, qy, qz);
+            const double a2 = PATH ? dev::dclamp(a1 + 0.5 * a.dalpha, 0.0, 1.0) : 0.0;
+            ok = dev::eval_at<MAXV, PATH, GR, true>(hex, c, a.L, a.V, a.f0, a.f1, qx, qy, qz, d, a2, hint0, hint1, sx, sy,
+                                                   sz, sw, coop, tile, th0, th1);
+            if (!ok) { died = (int)step; break; }
+            hx = hx + sx * 2.0; hy = hy + sy * 2.0; hz = hz + sz * 2.0; wv = wv + 2.0 * sw;
+            dev::advect((unsigned)step, x, y, z, sx, sy, sz, dt * 0.5, qx, qy, qz);
+            ok = dev::eval_at<MAXV, PATH, GR, true>(hex, c, a.L, a.V, a.f0, a.f1, qx, qy, qz, d, a2, hint0, hint1, sx, sy,
+                                                   sz, sw, coop, tile, th0, th1);
+            if (!ok) { died = (int)step; break; }
+            hx = hx + sx * 2.0; hy = hy + sy * 2.0; hz = hz + sz * 2.0; wv = wv + 2.0 * sw;
+            dev::advect((unsigned)step, x, y, z, sx, sy, sz, dt, qx, qy, qz);
+            const double a4 = PATH ? dev::dclamp(a1 + a.dalpha, 0.0, 1.0) : 0.0;
+            ok = dev::eval_at<MAXV, PATH, GR, true>(hex, c, a.L, a.V, a.f0, a.f1, qx, qy, qz, d, a4, hint0, hint1, sx, sy,
+                                                   sz, sw, coop, tile, th0, th1);
+            if (!ok) { died = (int)step; break; }
+            hx = (hx + sx) / 6.0; hy = (hy + sy) / 6.0; hz = (hz + sz) / 6.0; wv = (wv + sw) / 6.0;
+#else
+            double s1x, s1y, s1z, s1w, s2x, s2y, s2z, s2w, s3x, s3y, s3z, s3w, s4x, s4y, s4z, s4w;
+            double qx, qy, qz;
             bool ok = dev::eval_at<MAXV, PATH, GR, true>(hex, c, a.L, a.V, a.f0, a.f1, x, y, z, d, a1, hint0, hint1,
                                                         s1x, s1y, s1z, s1w, coop, tile, th0, th1);
             if (!ok) { died = (int)step; break; }
@@ -1867,6 +1981,7 @@ __global__ void __launch_bounds__(kTrajBlock, (TrajWaves<MAXV, PATH, EULER>::val
             hy = (((s1y + s2y * 2.0) + s3y * 2.0) + s4y) / 6.0;
             hz = (((s1z + s2z * 2.0) + s3z * 2.0) + s4z) / 6.0;
             wv = (s1w + 2.0 * s2w + 2.0 * s3w + s4w) / 6.0;
+#endif
             const double tx = x + hx * dt, ty = y + hy * dt, tz = z + hz * dt;
             const double tl = dev::len3(tx, ty, tz);
             if (tl > 1e-12) {
@@ -2421,7 +2536,8 @@ __global__ void vertex_bary_kernel(int64_t V, const int* __restrict__ cov, const
 template <int DIM>
 __global__ void cell_to_vertex_bary_kernel(int64_t V, int Lt, const int* __restrict__ cov,
                                            const double4* __restrict__ bary, const double* __restrict__ src,
-                                           double* __restrict__ dst, int clamp_neg) {
+                                           double* __restrict__ dst, int clamp_neg,
+                                           const int* __restrict__ vrow = nullptr) {
     const int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (idx >= V * Lt) return;
     const int64_t vid = idx / Lt;
@@ -2442,8 +2558,10 @@ __global__ void cell_to_vertex_bary_kernel(int64_t V, int Lt, const int* __restr
             out[d] = o;
         }
     }
+    // (vrow: internal vertex -> the caller's row, mops_cell_to_vertex_attr)
+    const int64_t o = vrow ? (int64_t)vrow[vid] * Lt + k : idx;
 #pragma unroll
-    for (int d = 0; d < DIM; ++d) dst[idx * DIM + d] = out[d];
+    for (int d = 0; d < DIM; ++d) dst[o * DIM + d] = out[d];
 }
 
 // ===========================================================================
@@ -2793,20 +2911,23 @@ template <typename IDX>
 __global__ void pair_record_kernel(int64_t V, int L, const double* __restrict__ zt, const double* __restrict__ vel,
                                    const double* __restrict__ w, double* __restrict__ pr) {
     const IDX j = (IDX)blockIdx.x * (IDX)blockDim.x + (IDX)threadIdx.x;
-    const IDX lm1 = (IDX)(L - 1);
     if ((int64_t)j >= V * (L - 1) * (kPairRec / 2)) return;
-    const IDX rec = j / (IDX)(kPairRec / 2);
-    const int q = (int)(j - rec * (IDX)(kPairRec / 2));
-#if MOPS_PR_LEVEL_MAJOR
+    // (k-1, q, v) with v fastest (piece-major: contiguous stores), or (k-1, v, q) record-major
     const IDX vv = (IDX)V;
-    const IDX kk = rec / vv;
-    const IDX v = rec - kk * vv;
-    const int k = (int)kk + 1;
-    (void)lm1;
-#else
-    const IDX v = rec / lm1;
-    const int k = (int)(rec - v * lm1) + 1;
-#endif
+    IDX v;
+    int q, k;
+    if (MOPS_PR_PIECES) {
+        const IDX r = j / vv;
+        v = j - r * vv;
+        q = (int)(r % (IDX)(kPairRec / 2));
+        k = (int)(r / (IDX)(kPairRec / 2)) + 1;
+    } else {
+        const IDX rec = j / (IDX)(kPairRec / 2);
+        q = (int)(j - rec * (IDX)(kPairRec / 2));
+        const IDX kk = rec / vv;
+        v = rec - kk * vv;
+        k = (int)kk + 1;
+    }
     double2 val;
     if (q == 0) {
         const double* z = zt + (int64_t)v * L;
@@ -2818,7 +2939,8 @@ __global__ void pair_record_kernel(int64_t V, int L, const double* __restrict__ 
         const double* u = vel + ((int64_t)v * L + k - 1) * 3 + 2 * (q - 2);
         val = make_double2(u[0], u[1]);
     }
-    reinterpret_cast<double2*>(pr)[j] = val;
+    reinterpret_cast<double2*>(pr)[pr_base((uint32_t)(k - 1), (uint32_t)v, (uint32_t)V) +
+                                   (uint32_t)q * pr_qstride((uint32_t)V)] = val;
 }
 
 // Level-major records ((k-1)*V + v) from the vertex-major zt/vel/w arrays: a block stages a
@@ -2832,6 +2954,9 @@ __global__ void pair_record_kernel(int64_t V, int L, const double* __restrict__ 
 #define MOPS_REC_TK 16
 #endif
 constexpr int kRecTV = MOPS_REC_TV, kRecTK = MOPS_REC_TK;
+#ifndef MOPS_REC_TILED
+#define MOPS_REC_TILED 1  // records built by pair_record_tiled_kernel (0: one 16-B piece per thread, pair_record_kernel)
+#endif
 __global__ void __launch_bounds__(256) pair_record_tiled_kernel(int64_t V, int L, const double* __restrict__ zt,
                                                                 const double* __restrict__ vel,
                                                                 const double* __restrict__ w,
@@ -2856,8 +2981,16 @@ __global__ void __launch_bounds__(256) pair_record_tiled_kernel(int64_t V, int L
     }
     __syncthreads();
     for (int i = t; i < nk * kRecTV * (kPairRec / 2); i += blockDim.x) {
-        const int rl = i / (kPairRec / 2), q = i - rl * (kPairRec / 2);
-        const int kl = rl / kRecTV, vl = rl - kl * kRecTV;
+        // piece-major: consecutive threads on consecutive vertices of one (level, piece) row
+        int q, kl, vl;
+        if (MOPS_PR_PIECES) {
+            vl = i % kRecTV;
+            const int r = i / kRecTV;
+            q = r % (kPairRec / 2); kl = r / (kPairRec / 2);
+        } else {
+            const int rl = i / (kPairRec / 2);
+            q = i - rl * (kPairRec / 2); kl = rl / kRecTV; vl = rl - kl * kRecTV;
+        }
         if (vl >= nv) continue;
         double2 val;
         if (q == 0) val = make_double2(sz[vl][kl], sz[vl][kl + 1]);
@@ -2865,8 +2998,8 @@ __global__ void __launch_bounds__(256) pair_record_tiled_kernel(int64_t V, int L
         else if (q == 2) val = make_double2(su[vl][kl][0], su[vl][kl][1]);
         else if (q == 3) val = make_double2(su[vl][kl][2], su[vl][kl + 1][0]);
         else val = make_double2(su[vl][kl + 1][1], su[vl][kl + 1][2]);
-        const int64_t rec = (int64_t)(k0 + kl) * V + v0 + vl;
-        reinterpret_cast<double2*>(pr)[rec * (kPairRec / 2) + q] = val;
+        reinterpret_cast<double2*>(pr)[pr_base((uint32_t)(k0 + kl), (uint32_t)(v0 + vl), (uint32_t)V) +
+                                       (uint32_t)q * pr_qstride((uint32_t)V)] = val;
     }
 }
 
@@ -2921,8 +3054,16 @@ __global__ void __launch_bounds__(256) pair_record_fused_kernel(int64_t V, int L
     }
     __syncthreads();
     for (int i = t; i < nk * kRecTV * (kPairRec / 2); i += blockDim.x) {
-        const int rl = i / (kPairRec / 2), q = i - rl * (kPairRec / 2);
-        const int kl = rl / kRecTV, vl = rl - kl * kRecTV;
+        // piece-major: consecutive threads on consecutive vertices of one (level, piece) row
+        int q, kl, vl;
+        if (MOPS_PR_PIECES) {
+            vl = i % kRecTV;
+            const int r = i / kRecTV;
+            q = r % (kPairRec / 2); kl = r / (kPairRec / 2);
+        } else {
+            const int rl = i / (kPairRec / 2);
+            q = i - rl * (kPairRec / 2); kl = rl / kRecTV; vl = rl - kl * kRecTV;
+        }
         if (vl >= nv) continue;
         double2 val;
         if (q == 0) val = make_double2(sz[vl][kl], sz[vl][kl + 1]);
@@ -2930,8 +3071,8 @@ __global__ void __launch_bounds__(256) pair_record_fused_kernel(int64_t V, int L
         else if (q == 2) val = make_double2(su[vl][kl][0], su[vl][kl][1]);
         else if (q == 3) val = make_double2(su[vl][kl][2], su[vl][kl + 1][0]);
         else val = make_double2(su[vl][kl + 1][1], su[vl][kl + 1][2]);
-        const int64_t rec = (int64_t)(k0 + kl) * V + v0 + vl;
-        reinterpret_cast<double2*>(pr)[rec * (kPairRec / 2) + q] = val;
+        reinterpret_cast<double2*>(pr)[pr_base((uint32_t)(k0 + kl), (uint32_t)(v0 + vl), (uint32_t)V) +
+                                       (uint32_t)q * pr_qstride((uint32_t)V)] = val;
     }
 }
 
@@ -2944,7 +3085,14 @@ __global__ void records_to_vertex_kernel(int64_t V, int L, const double* __restr
     const int64_t v = idx / L;
     const int j = (int)(idx - v * L);
     const bool hi = j == L - 1;  // the second half of record L-2
-    const double* r = pr + ((int64_t)(hi ? j - 1 : j) * V + v) * kPairRec;
+    const double2* p2 = reinterpret_cast<const double2*>(pr);
+    const uint32_t b = pr_base((uint32_t)(hi ? j - 1 : j), (uint32_t)v, (uint32_t)V), qs = pr_qstride((uint32_t)V);
+    double r[kPairRec];  // the record's 10 doubles in their order
+#pragma unroll
+    for (int q = 0; q < kPairRec / 2; ++q) {
+        const double2 x = p2[b + (uint32_t)q * qs];
+        r[2 * q] = x.x; r[2 * q + 1] = x.y;
+    }
     w[v * (L + 1) + j] = hi ? r[3] : r[2];
     vel[idx * 3 + 0] = hi ? r[7] : r[4];
     vel[idx * 3 + 1] = hi ? r[8] : r[5];
@@ -3063,6 +3211,24 @@ mops_status dmalloc(T** p, size_t count, int64_t* acc) {
 
 inline unsigned grid_for(int64_t n) { return (unsigned)((n + kBlock - 1) / kBlock); }
 
+// 63-bit Morton key of a vertex direction (the cell_key_kernel quantisation, on the host)
+uint64_t vertex_morton_key(double x, double y, double z) {
+    auto spread = [](uint64_t v) {
+        v &= 0x1fffffULL;
+        v = (v | (v << 32)) & 0x1f00000000ffffULL;
+        v = (v | (v << 16)) & 0x1f0000ff0000ffULL;
+        v = (v | (v << 8)) & 0x100f00f00f00f00fULL;
+        v = (v | (v << 4)) & 0x10c30c30c30c30c3ULL;
+        v = (v | (v << 2)) & 0x1249249249249249ULL;
+        return v;
+    };
+    const double r = std::sqrt(x * x + y * y + z * z);
+    const double sc = (r > 0.0 && std::isfinite(r)) ? 1.0 / r : 0.0;
+    const double m = 2097151.0;
+    auto q = [&](double a) { return (uint64_t)std::fmin(std::fmax((a * sc * 0.5 + 0.5) * m, 0.0), m); };
+    return (spread(q(x)) << 2) | (spread(q(y)) << 1) | spread(q(z));
+}
+
 int pick_maxv(int maxE) {
     if (maxE <= 7) return 7;
     if (maxE <= 12) return 12;
@@ -3094,6 +3260,7 @@ void free_mesh(mops_mesh* m) {
     (void)hipFree(m->d_eoc); (void)hipFree(m->d_coe); (void)hipFree(m->d_exyz); (void)hipFree(m->d_rbf_coef);
     (void)hipFree(m->d_rbf_slot);
     for (auto& f : m->coop_flags) (void)hipFree(f.second);
+    (void)hipFree(m->d_vold);
     delete m;
 }
 
@@ -3288,6 +3455,8 @@ mops_status mops_mesh_create(const mops_mesh_desc* desc, void* stream, mops_mesh
     // level-pair record indices are 32-bit (dev::pair_sums): V*(L-1) + 1 records < 2^31
     if (V * (int64_t)L >= INT32_MAX)
         return fail(MOPS_ERR_UNSUPPORTED, "mops_mesh_create: nVertices * nVertLevels >= 2^31");
+    if (L >= 2 && pr_pieces(V, L) >= ((uint64_t)1 << 32))  // 32-bit record piece indices (pr_base)
+        return fail(MOPS_ERR_UNSUPPORTED, "mops_mesh_create: 5 (nVertices + 1) (nVertLevels - 1) >= 2^32");
     if (C > ((int64_t)1 << 30))  // the bucket directory's 32-bit size doubles up to 2C slots
         return fail(MOPS_ERR_UNSUPPORTED, "mops_mesh_create: nCells > 2^30");
     if (!desc->h_n_edges_on_cell || !desc->h_vertices_on_cell || !desc->h_cells_on_cell || !desc->h_cell_coord ||
@@ -3298,6 +3467,20 @@ mops_status mops_mesh_create(const mops_mesh_desc* desc, void* stream, mops_mesh
     m->C = C; m->V = V; m->maxE = maxE; m->L = L;
     m->maxv = pick_maxv(maxE);
     m->rec_ints = rec_ints_for(m->maxv);
+    // ---- vertex numbering (MOPS_VPERM): the Morton order of the vertex coordinates, so the vertices of
+    // neighbouring cells -- the level-pair records one gather instruction asks for -- are close in memory
+    std::vector<int> vnew;  // caller's vertex -> internal (empty = identity)
+    if (MOPS_VPERM) {
+        const double* h = desc->h_vertex_coord;
+        std::vector<std::pair<uint64_t, int>> key((size_t)V);
+        for (int64_t v = 0; v < V; ++v) key[v] = {vertex_morton_key(h[3 * v], h[3 * v + 1], h[3 * v + 2]), (int)v};
+        std::sort(key.begin(), key.end());
+        m->h_vold.resize((size_t)V);
+        vnew.resize((size_t)V);
+        for (int64_t i = 0; i < V; ++i) { m->h_vold[i] = key[i].second; vnew[key[i].second] = (int)i; }
+    }
+    auto vin = [&](int64_t v) -> int64_t { return vnew.empty() ? v : (int64_t)vnew[v]; };  // caller -> internal
+    auto vout = [&](int64_t i) -> int64_t { return m->h_vold.empty() ? i : (int64_t)m->h_vold[i]; };  // internal -> caller
     // ---- cell records (validated) ----
     std::vector<int> rec((size_t)C * m->rec_ints, -1);
     m->h_nv.reserve((size_t)C);
@@ -3315,7 +3498,7 @@ mops_status mops_mesh_create(const mops_mesh_desc* desc, void* stream, mops_mesh
                     free_mesh(m);
                     return fail(MOPS_ERR_INVALID, "verticesOnCell entry out of range for an active edge");
                 }
-                r[1 + k] = (int)(v1 - 1);
+                r[1 + k] = (int)vin((int64_t)(v1 - 1));
             }
             // walk candidates: the reference skips cid < 0 || cid >= C (:910)
             r[1 + m->maxv + k] = (c1 >= 1 && c1 <= (uint64_t)C) ? (int)(c1 - 1) : -1;
@@ -3360,11 +3543,19 @@ mops_status mops_mesh_create(const mops_mesh_desc* desc, void* stream, mops_mesh
         if (e2 == hipSuccess) e2 = hipStreamSynchronize(s);
         if (e2 != hipSuccess) { free_mesh(m); return fail(MOPS_ERR_HIP, hipGetErrorString(e2)); }
     }
-    if ((st = upload_xyz(desc->h_vertex_coord, V, &m->d_vxyz, &acc, s)) != MOPS_OK) { free_mesh(m); return st; }
+    {
+        std::vector<double> vc((size_t)V * 3);
+        for (int64_t i = 0; i < V; ++i)
+            for (int d = 0; d < 3; ++d) vc[3 * i + d] = desc->h_vertex_coord[3 * vout(i) + d];
+        if ((st = upload_xyz(vc.data(), V, &m->d_vxyz, &acc, s)) != MOPS_OK) { free_mesh(m); return st; }
+    }
+    if (!m->h_vold.empty()) {
+        if ((st = upload(m->h_vold.data(), m->h_vold.size(), &m->d_vold, &acc, s)) != MOPS_OK) { free_mesh(m); return st; }
+    }
     if (desc->h_cells_on_vertex) {
         std::vector<int> cov((size_t)V * 3);
         for (int64_t i = 0; i < V * 3; ++i) {
-            const uint64_t x = desc->h_cells_on_vertex[i];
+            const uint64_t x = desc->h_cells_on_vertex[3 * vout(i / 3) + i % 3];
             // reference boundary test: (x - 1) > C + 1 as size_t (Q10); ids C, C+1
             // would read out of range there -- rejected here
             if (x == 0 || x - 1 > (uint64_t)(C + 1)) cov[i] = -1;
@@ -3542,11 +3733,23 @@ mops_status mops_cell_center_velocity_rbf(const mops_mesh* m, const double* d_no
     return MOPS_OK;
 }
 
+// the all-zero record's pieces (pair_sums reads it for slots v >= nv): vertex V of every (layer, piece) row
+// (piece-major) or the record after the last (record-major); the builders never write them
+__global__ void pr_zero_kernel(int64_t V, int L, double2* __restrict__ pr) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (MOPS_PR_PIECES) {
+        if (i < (int64_t)(L - 1) * (kPairRec / 2)) pr[(uint64_t)i * (uint64_t)(V + 1) + (uint64_t)V] = make_double2(0.0, 0.0);
+    } else if (i < kPairRec / 2) {
+        pr[pr_zero((uint32_t)V, (uint32_t)L) + (uint32_t)i] = make_double2(0.0, 0.0);
+    }
+}
+
 static mops_status alloc_records(const mops_mesh* mesh, mops_field* f, hipStream_t s) {
-    const int64_t npr = mesh->V * (int64_t)std::max(mesh->L - 1, 0);
-    // + one all-zero record at index npr: pair_sums reads it for v >= nv
-    if (!f->d_pr) MOPS_TRY(dmalloc(&f->d_pr, (size_t)((npr + 1) * kPairRec), &f->bytes));
-    HIP_TRY(hipMemsetAsync(f->d_pr + npr * kPairRec, 0, kPairRec * sizeof(double), s));
+    if (mesh->L < 2) return MOPS_OK;
+    if (!f->d_pr) MOPS_TRY(dmalloc(&f->d_pr, (size_t)(pr_pieces(mesh->V, mesh->L) * 2), &f->bytes));
+    pr_zero_kernel<<<grid_for((int64_t)(mesh->L - 1) * (kPairRec / 2)), kBlock, 0, s>>>(
+        mesh->V, mesh->L, reinterpret_cast<double2*>(f->d_pr));
+    HIP_TRY(hipGetLastError());
     return MOPS_OK;
 }
 
@@ -3556,7 +3759,7 @@ static mops_status compute_flags(const mops_mesh* mesh, mops_field* f, hipStream
 static mops_status compute_mono(const mops_mesh* mesh, mops_field* f, hipStream_t s) {
     const int64_t npr = mesh->V * (int64_t)std::max(mesh->L - 1, 0);
     MOPS_TRY(alloc_records(mesh, f, s));
-#if MOPS_PR_LEVEL_MAJOR
+#if MOPS_REC_TILED
     if (npr > 0) {
         const dim3 grid((unsigned)((mesh->V + kRecTV - 1) / kRecTV), (unsigned)((mesh->L - 1 + kRecTK - 1) / kRecTK));
         pair_record_tiled_kernel<<<grid, 256, 0, s>>>(mesh->V, mesh->L, f->d_zt, f->d_vel, f->d_w, f->d_pr);
@@ -3599,6 +3802,19 @@ mops_status mops_field_create_derived(const mops_mesh* mesh, const double* h_zt,
     f->mesh = mesh; f->V = mesh->V; f->L = mesh->L;
     const size_t V = (size_t)mesh->V, L = (size_t)mesh->L;
     mops_status st;
+    // the caller's vertex rows in the internal vertex order (mops_mesh::h_vold)
+    std::vector<double> pzt, pvel, pw;
+    if (!mesh->h_vold.empty()) {
+        auto perm = [&](const double* src, size_t row, std::vector<double>& dst) {
+            dst.resize(V * row);
+            for (size_t i = 0; i < V; ++i)
+                std::memcpy(dst.data() + i * row, src + (size_t)mesh->h_vold[i] * row, row * sizeof(double));
+            return dst.data();
+        };
+        h_zt = perm(h_zt, L, pzt);
+        h_vel = perm(h_vel, L * 3, pvel);
+        if (h_w) h_w = perm(h_w, L + 1, pw);
+    }
     if ((st = upload(h_zt, V * L, &f->d_zt, &f->bytes, s)) != MOPS_OK ||
         (st = upload(h_vel, V * L * 3, &f->d_vel, &f->bytes, s)) != MOPS_OK) { free_field(f); return st; }
     if (h_w) {
@@ -3669,7 +3885,7 @@ static mops_status field_derive(const mops_mesh* mesh, mops_field* f, const mops
     } else {  // edge normals only: the RBF reconstruction (MPASOSolution::calcCellCenterVelocity)
         MOPS_TRY(mops_cell_center_velocity_rbf(mesh, d->h_normal_velocity, velc, s));
     }
-#if MOPS_PR_LEVEL_MAJOR && MOPS_FUSED_RECORDS
+#if MOPS_FUSED_RECORDS
     if (L >= 2) {
         // CalcCellVertexZtop / CalcCellVertexVelocity / CalcCellVertexVertVelocity fused into the
         // level-pair record build (pair_record_fused_kernel)
@@ -3762,7 +3978,7 @@ mops_status mops_cell_to_vertex_attr(const mops_mesh* mesh, const double* d_cell
         return fail(MOPS_ERR_INVALID, "mops_cell_to_vertex_attr: null argument");
     hipStream_t s = (hipStream_t)stream;
     cell_to_vertex_bary_kernel<1><<<grid_for(mesh->V * mesh->L), kBlock, 0, s>>>(
-        mesh->V, mesh->L, mesh->d_cov, mesh->d_bary, d_cell_attr, d_vertex_attr, 1);
+        mesh->V, mesh->L, mesh->d_cov, mesh->d_bary, d_cell_attr, d_vertex_attr, 1, mesh->d_vold);
     HIP_TRY(hipGetLastError());
     return MOPS_OK;
 }
@@ -3778,6 +3994,18 @@ mops_status mops_field_export(const mops_field* f, double* h_zt, double* h_vel, 
     if (h_vel) HIP_TRY(hipMemcpyAsync(h_vel, f->d_vel, V * L * 3 * sizeof(double), hipMemcpyDeviceToHost, s));
     if (h_w) HIP_TRY(hipMemcpyAsync(h_w, f->d_w, V * (L + 1) * sizeof(double), hipMemcpyDeviceToHost, s));
     HIP_TRY(hipStreamSynchronize(s));
+    const std::vector<int>& vold = f->mesh->h_vold;  // internal rows -> the caller's vertex order
+    if (!vold.empty()) {
+        std::vector<double> tmp;
+        auto unperm = [&](double* buf, size_t row) {
+            tmp.assign(buf, buf + V * row);
+            for (size_t i = 0; i < V; ++i)
+                std::memcpy(buf + (size_t)vold[i] * row, tmp.data() + i * row, row * sizeof(double));
+        };
+        if (h_zt) unperm(h_zt, L);
+        if (h_vel) unperm(h_vel, L * 3);
+        if (h_w) unperm(h_w, L + 1);
+    }
     return MOPS_OK;
 }
 

@@ -216,6 +216,23 @@ class RecordGather:
         self.bytes_per_rank += (K * 6 + 4) * self.stride * 8
         return self.done
 
+    def plan(self) -> dict:
+        """The per-rank memory plan of the collection (bench.py prints it for N > 1): bytes gathered per
+        checkpoint (every rank's slab at the longest record count), the ring that receives them (the whole
+        gathered slab, or chunks of records when max_bytes bounds it), the spare slab and aux buffers, and
+        the HBM left beside the fields once they are allocated."""
+        per_rec = self.world * 6 * self.stride * 8
+        out = {"world": self.world, "records_per_checkpoint_max": self.shape[0],
+               "gathered_bytes_per_checkpoint": per_rec * self.shape[0],
+               "sent_bytes_per_checkpoint": (self.shape[0] * 6 + 4) * self.stride * 8,
+               "ring_bytes": self.gathered.numel() * 8 + self.gathered_aux.numel() * 8,
+               "ring_records": self.chunk, "chunked": self.chunk < self.shape[0],
+               "spare_slab_bytes": self.spare.numel() * 8, "aux_bytes": sum(a.numel() for a in self.aux) * 8}
+        if self.cuda:
+            free, total = self.torch.cuda.mem_get_info(self.spare.device)
+            out.update(hbm_free_bytes=int(free), hbm_total_bytes=int(total))
+        return out
+
     def synchronize(self):
         if self.cuda and self.comm is not None:
             self.comm.synchronize()

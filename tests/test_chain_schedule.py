@@ -151,6 +151,9 @@ def _gather_worker(rank, world, port, q, ring_records=1):
         ring.collect(shard2)
         want = [(k0, min(K, k0 + ring_records)) for k0 in range(0, K, ring_records)]
         ok &= ring.chunk == min(ring_records, kmax) and [c[:2] for c in chunks] == want
+        pl = ring.plan()  # the memory plan bench.py prints for N > 1
+        ok &= (pl["gathered_bytes_per_checkpoint"] == world * kmax * 6 * npad * 8 and pl["chunked"] == (ring.chunk < kmax)
+               and pl["ring_bytes"] == world * (ring.chunk * 6 + 4) * npad * 8)
         whole = coll.gathered.view(-1)[: world * K * 6 * npad].view(world, K, 6, npad)
         ok &= torch.equal(torch.cat([c[2] for c in chunks], 1), whole)
         # the first pair's 4 records through the same ring: a ragged last chunk when ring_records = 3

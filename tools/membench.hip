@@ -120,6 +120,24 @@ __global__ void __launch_bounds__(256) mb_l1_partial(const double2* __restrict__
     out[(int64_t)blockIdx.x * blockDim.x + threadIdx.x] = s;
 }
 
+// does the TD cost of a wave-instruction grow with the distinct cache lines its lanes touch?  Each block
+// re-reads its own 8 KiB (512 x 16 B, L1-resident at 2 blocks per CU); lane j reads piece
+// (j * stride + k) & 511: stride 1 = 64 consecutive pieces (8 lines of 128 B), 2 = 16 lines, 4 = 32, 8 = 64
+// (one line per lane) -- the trajectory kernel's record gathers are the last case
+__global__ void __launch_bounds__(256) mb_l1_scatter(const double2* __restrict__ a, int iters, int stride, double* out) {
+    const double2* base = a + (int64_t)blockIdx.x * 512;
+    const int j = threadIdx.x & 63, w = threadIdx.x >> 6;
+    double s = 0.0;
+    for (int k = 0; k < iters; k += 4) {
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+            const double2 v = base[(j * stride + 64 * (w + u) + k) & 511];
+            s += v.x + v.y;
+        }
+    }
+    out[(int64_t)blockIdx.x * blockDim.x + threadIdx.x] = s;
+}
+
 static float time_ms(hipEvent_t a, hipEvent_t b) {
     float ms = 0.f;
     CK(hipEventElapsedTime(&ms, a, b));
@@ -224,6 +242,26 @@ int main(int argc, char** argv) {
         }
     }
     CK(hipFree(l1));
+    // 6. scattered L1-resident re-reads (mb_l1_scatter): 2 blocks per CU, 8 KiB each
+    {
+        const int nb2 = ncu * 2;
+        double2* sc = nullptr;
+        CK(hipMalloc(&sc, (int64_t)nb2 * 512 * 16));
+        CK(hipMemset(sc, 0, (int64_t)nb2 * 512 * 16));
+        for (int stride = 1; stride <= 8; stride *= 2) {
+            for (int r = 0; r < reps; ++r) {
+                CK(hipEventRecord(e0));
+                mb_l1_scatter<<<nb2, 256>>>(sc, iters, stride, out);
+                CK(hipEventRecord(e1));
+                CK(hipEventSynchronize(e1));
+                printf("{\"kernel\": \"mb_l1_scatter\", \"stride\": %d, \"lines_per_instr\": %d, \"rep\": %d, "
+                       "\"ms\": %.4f, \"wave_instrs\": %lld, \"lane_bytes\": %lld, \"cus\": %d}\n", stride,
+                       8 * stride, r, time_ms(e0, e1), (long long)nb2 * 4 * iters, (long long)nb2 * 256 * iters * 16ll,
+                       ncu);
+            }
+        }
+        CK(hipFree(sc));
+    }
     CK(hipFree(out));
     return 0;
 }
