@@ -183,6 +183,8 @@ struct mops_mesh {
     int2* d_hval = nullptr;       // [H]
     uint32_t hmask = 0;           // H - 1
     uint32_t* d_cell_rank = nullptr;  // rank of each cell in the Morton order of the centres (particle locality order)
+    int* d_rank_cell = nullptr;       // the inverse: the cell of each rank
+    double2* d_cpolyr = nullptr;      // [2*7][C] d_cpoly's pieces by cell rank (maxv 7 meshes; MOPS_CPOLY_RANK)
     // [C][maxv] each cell's polygon in rotated slot order with its Wachspress weights' numerators:
     // slot j = {poly[j-1] (poly[-1] = poly[nv-1]), B_j = area(poly[j-1], poly[j], poly[j+1])}, zeros past nv
     double4* d_cpoly = nullptr;
@@ -565,6 +567,12 @@ __device__ __forceinline__ double dclamp(double v, double lo, double hi) { retur
 #ifndef MOPS_CPOLY
 #define MOPS_CPOLY 1
 #endif
+// ... and (MAXV 7) read it piece-major in the cells' Morton-rank order, mops_mesh::d_cpolyr [14][C]: the lanes of a
+// wave sit in consecutive-rank cells (the particles' locality order), so one polygon-piece gather touches a few
+// 128-B lines instead of one per cell (the TD spends a cycle per line)
+#ifndef MOPS_CPOLY_RANK
+#define MOPS_CPOLY_RANK 1
+#endif
 
 // Per-cell stencil cached in registers while the particle stays in the cell.
 template <int MAXV>
@@ -594,6 +602,9 @@ struct Cell {
     float* rb2;      // MOPS_LDS_COMPACT: the pair test's rb2 (else pr2[4 * kTrajBlock])
     const double4* __restrict__ vxyz;   // rc == false: polygon re-read per evaluation (L1-resident)
     const double4* __restrict__ cpoly;  // rc == false: per-cell rotated polygon + B_i [C][MAXV] (cell_poly_kernel)
+    const double2* __restrict__ cpolyr;  // MOPS_CPOLY_RANK: the same, piece-major by cell rank [2 MAXV][C]
+    const uint32_t* __restrict__ crank;  // mops_mesh::d_cell_rank
+    uint32_t rank, C;                    // this cell's rank (load_cell), the cell count
 };
 
 // NRMC (the cooperative kernel): the lane's normals, when it keeps them (c.lds_n, a wave-uniform
@@ -634,6 +645,7 @@ __device__ __forceinline__ void load_cell(Cell<MAXV>& c, int cell, const int* __
     if constexpr (!RC) {
         c.vxyz = vxyz;
         c.cpoly = cpoly;
+        if constexpr (MOPS_CPOLY_RANK && MAXV == 7) c.rank = c.crank[cell];
     }
     if constexpr (NRMC) {
         if (c.lds_n) {
@@ -730,8 +742,15 @@ __device__ __forceinline__ bool weights(const Cell<MAXV>& c, int L, int V, doubl
                 // one 32-B slot {x, y, z, B_j} of the cell's packed polygon: 2 VMEM instead of 3; in a
                 // cooperative wave (coop, wave-uniform) the same slot from the wave's LDS tile
                 double4 q;
-                if constexpr (COOP) q = tpoly[j];
-                else q = c.cpoly[(int64_t)c.id * MAXV + j];
+                if constexpr (COOP) {
+                    q = tpoly[j];
+                } else if constexpr (MOPS_CPOLY_RANK && MAXV == 7) {
+                    const double2 lo = c.cpolyr[(uint32_t)(2 * j) * c.C + c.rank];
+                    const double2 hi = c.cpolyr[(uint32_t)(2 * j + 1) * c.C + c.rank];
+                    q = make_double4(lo.x, lo.y, hi.x, hi.y);
+                } else {
+                    q = c.cpoly[(int64_t)c.id * MAXV + j];
+                }
                 X[j] = q.x; Y[j] = q.y; Z[j] = q.z; BB[j] = q.w;
 #else
                 const double4 q = c.vxyz[j == 0 ? c.vlast : c.vid[(j + MAXV - 1) % MAXV]];
@@ -1300,9 +1319,11 @@ __device__ __forceinline__ void pair_sums(const Cell<MAXV>& c, const double* w, 
 #pragma unroll
                     for (int q = 0; q < kPairRec / 2; ++q) a[j][q] = trec[(kPairRec / 2) * v + q];
                 } else {
-                    const double2* r = reinterpret_cast<const double2*>(pr);
+                    // (a 64-bit base, then the pieces at q * qs: with record-major records (qs = 1) the five loads
+                    // share one address and take immediate offsets)
+                    const double2* r = reinterpret_cast<const double2*>(pr) + ri;
 #pragma unroll
-                    for (int q = 0; q < kPairRec / 2; ++q) a[j][q] = r[ri + (uint32_t)q * qs];
+                    for (int q = 0; q < kPairRec / 2; ++q) a[j][q] = r[(size_t)q * qs];
                 }
             }
 #pragma unroll
@@ -1496,6 +1517,8 @@ struct TrajArgs {
     const double4* __restrict__ cpoly;  // per-cell rotated polygon + Wachspress B_i (mops_mesh::d_cpoly)
     const double* __restrict__ cnrm;    // per-cell edge normals (mops_mesh::d_cnrm; NULL past maxEdges 7)
     const uint4* __restrict__ nbr;      // per-cell neighbour table (mops_mesh::d_nbr; NULL past maxEdges 7)
+    const double2* __restrict__ cpolyr;  // mops_mesh::d_cpolyr (NULL past maxEdges 7)
+    const uint32_t* __restrict__ crank;  // mops_mesh::d_cell_rank
     const int* __restrict__ coop_sel;   // per-launch device flag: 1 = the cooperative instantiation runs, 0 = the
                                         // plain one (the other exits at once); NULL = no selection
     double* px; double* py; double* pz;
@@ -1637,6 +1660,9 @@ __global__ void __launch_bounds__(kTrajBlock, (TrajWaves<MAXV, PATH, EULER, COOP
     c.id = -1;
     c.nv = 0;
     c.V = a.V;
+    c.cpolyr = a.cpolyr;
+    c.crank = a.crank;
+    c.C = (uint32_t)a.C;
     // cooperative waves (see kTilePieces): the wave's LDS tile and its group headers; their kernel keeps no
     // per-lane normals (a tiled wave reads its cells' normals from the tile, any other wave computes them)
     // (RK4 too: its four stages are evaluated in the step's start cell, quirk Q1, so a group's polygon and
@@ -2850,6 +2876,15 @@ __global__ void cell_nbr_kernel(int64_t C, const int* __restrict__ cellrec, cons
     for (int j = 0; j < kNbrQ; ++j) nbr[c * kNbrQ + j] = make_uint4(w[4 * j], w[4 * j + 1], w[4 * j + 2], w[4 * j + 3]);
 }
 
+// d_cpoly's 16-B pieces by cell rank: piece p (slot p / 2, half p % 2) of the cell of rank r at p * C + r
+__global__ void cpoly_rank_kernel(int64_t C, const int* __restrict__ rank_cell, const double4* __restrict__ cpoly,
+                                  double2* __restrict__ cpolyr) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= C * 14) return;
+    const int64_t p = i / C, r = i - p * C;
+    cpolyr[i] = reinterpret_cast<const double2*>(cpoly)[(int64_t)rank_cell[r] * 14 + p];
+}
+
 // Each cell's polygon in the evaluation's rotated slot order (dev::Cell: slot j holds
 // poly[j-1], slot 0 poly[nv-1]) packed with its Wachspress numerator B_j = area(poly[j-1],
 // poly[j], poly[j+1]) -- the same device arithmetic as the in-kernel computation, so
@@ -3255,7 +3290,7 @@ void free_mesh(mops_mesh* m) {
     if (!m) return;
     (void)hipFree(m->d_cellrec); (void)hipFree(m->d_cxyz); (void)hipFree(m->d_vxyz); (void)hipFree(m->d_cov);
     (void)hipFree(m->d_bary);
-    (void)hipFree(m->d_bkeys); (void)hipFree(m->d_bcells); (void)hipFree(m->d_hkeys); (void)hipFree(m->d_hval); (void)hipFree(m->d_cell_rank); (void)hipFree(m->d_cpoly); (void)hipFree(m->d_cnrm); (void)hipFree(m->d_nbr); (void)hipFree(m->d_rloc2); (void)hipFree(m->d_ring);
+    (void)hipFree(m->d_bkeys); (void)hipFree(m->d_bcells); (void)hipFree(m->d_hkeys); (void)hipFree(m->d_hval); (void)hipFree(m->d_cell_rank); (void)hipFree(m->d_rank_cell); (void)hipFree(m->d_cpolyr); (void)hipFree(m->d_cpoly); (void)hipFree(m->d_cnrm); (void)hipFree(m->d_nbr); (void)hipFree(m->d_rloc2); (void)hipFree(m->d_ring);
     (void)hipFree(m->d_scratch);
     (void)hipFree(m->d_eoc); (void)hipFree(m->d_coe); (void)hipFree(m->d_exyz); (void)hipFree(m->d_rbf_coef);
     (void)hipFree(m->d_rbf_slot);
@@ -3624,7 +3659,9 @@ mops_status mops_mesh_create(const mops_mesh_desc* desc, void* stream, mops_mesh
             cell_rank_kernel<<<grid_for(C), kBlock, 0, s>>>(C, cid_sorted, m->d_cell_rank);
             e = hipStreamSynchronize(s);
         }
-        (void)hipFree(ck); (void)hipFree(ck_sorted); (void)hipFree(cid); (void)hipFree(cid_sorted); (void)hipFree(ctmp);
+        (void)hipFree(ck); (void)hipFree(ck_sorted); (void)hipFree(cid); (void)hipFree(ctmp);
+        m->d_rank_cell = cid_sorted;  // kept: the cell of each rank (cpoly_rank_kernel)
+        acc += C * (int64_t)sizeof(int);
         if (e != hipSuccess) { free_mesh(m); return fail(MOPS_ERR_HIP, std::string("cell rank sort: ") + hipGetErrorString(e)); }
     }
     if ((st = dmalloc(&m->d_rloc2, (size_t)C, &acc)) != MOPS_OK) { free_mesh(m); return st; }
@@ -3647,7 +3684,13 @@ mops_status mops_mesh_create(const mops_mesh_desc* desc, void* stream, mops_mesh
     if (m->maxv == 7 && (st = dmalloc(&m->d_nbr, (size_t)(C * kNbrQ), &acc)) != MOPS_OK) { free_mesh(m); return st; }
     if (m->maxv == 7) cell_nbr_kernel<<<grid_for(C), kBlock, 0, s>>>(C, m->d_cellrec, m->d_cxyz, m->d_nbr);
     switch (m->maxv) {
-        case 7: cell_poly_kernel<7><<<grid_for(C), kBlock, 0, s>>>(C, m->d_cellrec, m->d_vxyz, m->d_cpoly, m->d_cnrm); break;
+        case 7:
+            cell_poly_kernel<7><<<grid_for(C), kBlock, 0, s>>>(C, m->d_cellrec, m->d_vxyz, m->d_cpoly, m->d_cnrm);
+            if (MOPS_CPOLY_RANK) {
+                if ((st = dmalloc(&m->d_cpolyr, (size_t)(C * 14), &acc)) != MOPS_OK) { free_mesh(m); return st; }
+                cpoly_rank_kernel<<<grid_for(C * 14), kBlock, 0, s>>>(C, m->d_rank_cell, m->d_cpoly, m->d_cpolyr);
+            }
+            break;
         case 12: cell_poly_kernel<12><<<grid_for(C), kBlock, 0, s>>>(C, m->d_cellrec, m->d_vxyz, m->d_cpoly); break;
         default: cell_poly_kernel<20><<<grid_for(C), kBlock, 0, s>>>(C, m->d_cellrec, m->d_vxyz, m->d_cpoly); break;
     }
@@ -4203,6 +4246,8 @@ mops_status mops_traj_advance(const mops_mesh* mesh, const mops_field* front, co
     a.cpoly = mesh->d_cpoly;
     a.cnrm = mesh->d_cnrm;
     a.nbr = mesh->d_nbr;
+    a.cpolyr = mesh->d_cpolyr;
+    a.crank = mesh->d_cell_rank;
     a.px = p->d_x; a.py = p->d_y; a.pz = p->d_z; a.depth = p->d_depth; a.cell = p->d_cell; a.death = p->d_death_step;
     a.n = p->n;
     a.step_begin = step_begin; a.step_end = step_end; a.n_steps = n_steps;
