@@ -1588,6 +1588,13 @@ struct RCache {
 #ifndef MOPS_NRM_PE
 #define MOPS_NRM_PE 1
 #endif
+#ifndef MOPS_NRM_PE_PLAIN
+// the plain (not cooperative) pathline Euler kernel, which runs the sparse waves of config 4, computes its
+// normals per evaluation instead: since the neighbour-table test the per-cell LDS column no longer pays --
+// config 4 2841 -> 2797 ms per 6-pair chain (3 interleaved rounds), config-2 mesh pathline 38.2-38.8 ms
+// either way (profiles/r05/ab/plain_kernel_normals.txt)
+#define MOPS_NRM_PE_PLAIN 0
+#endif
 #ifndef MOPS_NRM_SR
 #define MOPS_NRM_SR 1  // with MOPS_W_SR 2 capping it at 256 VGPRs: 86.3-87.0 vs 88.6-89.2 ms (config-2 mesh)
 #endif
@@ -1670,7 +1677,7 @@ __global__ void __launch_bounds__(kTrajBlock, (TrajWaves<MAXV, PATH, EULER, COOP
     // (MOPS_RC_PE_PLAIN: the plain -- not cooperative -- pathline Euler kernel, which runs the sparse waves of
     // config 4, keeps the polygon in registers: 12 fewer VMEM per evaluation for a TD-bound launch)
     constexpr bool kRC = RCache<MAXV, PATH, EULER>::value || (MOPS_RC_PE_PLAIN && PATH && EULER && !COOP && MAXV <= 7),
-                   kNrm = LdsNormals<MAXV, PATH, EULER>::value;
+                   kNrm = LdsNormals<MAXV, PATH, EULER>::value && (MOPS_NRM_PE_PLAIN || COOP || !PATH || !EULER);
     constexpr bool kCoop = COOP && PATH && MAXV == 7 && !kRC && kNrm && MOPS_CPOLY &&
                            (EULER ? MOPS_COOP_PE : MOPS_COOP_PR);
     // the tile and its headers are per block, and the group/header hand-offs between lanes rely on one
