@@ -2241,6 +2241,20 @@ __global__ void __launch_bounds__(256) assemble_kernel(int64_t n, int64_t K, con
 // once, with consecutive threads on consecutive doubles of a line (whole 600-B point runs at K =
 // 24 instead of 192-B chunks), saving remove_nan_kernel's second, strided pass over the lines.
 constexpr int kAsmFull = 24;
+#ifndef MOPS_ASM_V2
+// 16-B record reads (even stride, full blocks) and streaming (non-temporal) line stores: config 3's per-pair
+// assembly 9.71 -> 8.46 ms, its 7-pair chain 3620 -> 3610 ms (3 interleaved rounds,
+// profiles/r05/ab/assembly_v2.txt)
+#define MOPS_ASM_V2 1
+#endif
+template <typename T>
+__device__ __forceinline__ void asm_store(T* p, T v) {
+#if MOPS_ASM_V2
+    __builtin_nontemporal_store(v, p);
+#else
+    *p = v;
+#endif
+}
 __global__ void __launch_bounds__(256) assemble_clean_kernel(int64_t n, int K, const double* __restrict__ seeds,
                                                              const double* __restrict__ rec, int64_t stride,
                                                              int pathline, const int32_t* __restrict__ line,
@@ -2255,6 +2269,16 @@ __global__ void __launch_bounds__(256) assemble_clean_kernel(int64_t n, int K, c
     const int64_t s0 = (int64_t)blockIdx.x * kAsmSlots;
     const int ns = (int)((n - s0) < kAsmSlots ? (n - s0) : kAsmSlots);
     const int P = K + 1;
+#if MOPS_ASM_V2
+    if (ns == kAsmSlots && (stride & 1) == 0) {  // (block-uniform) 16-B pieces: 2 slots per load
+        for (int e = t; e < K * 6 * (kAsmSlots / 2); e += blockDim.x) {
+            const int i2 = e % (kAsmSlots / 2), c = (e / (kAsmSlots / 2)) % 6, kk = e / ((kAsmSlots / 2) * 6);
+            const double2 v = *reinterpret_cast<const double2*>(rec + kk * 6 * stride + c * stride + s0 + 2 * i2);
+            tile[kk][c][2 * i2] = v.x;
+            tile[kk][c][2 * i2 + 1] = v.y;
+        }
+    } else
+#endif
     for (int e = t; e < K * 6 * kAsmSlots; e += blockDim.x) {
         const int i = e % kAsmSlots, c = (e / kAsmSlots) % 6, kk = e / (kAsmSlots * 6);
         if (i < ns) tile[kk][c][i] = rec[kk * 6 * stride + c * stride + s0 + i];
@@ -2275,22 +2299,22 @@ __global__ void __launch_bounds__(256) assemble_clean_kernel(int64_t n, int K, c
     for (int e = t; e < ns * P * 3; e += blockDim.x) {  // points (and velocities)
         const int i = e / (P * 3), off = e - i * (P * 3), j = off / 3, c = off - j * 3, k = cut[i];
         const int64_t o = 3 * row[i] * P + off;
-        pts[o] = (k < P && (k == 0 || j >= k)) ? point(i, k == 0 ? 0 : k - 1, c) : point(i, j, c);
-        if (vel) vel[o] = (j == K || (k < P && (k == 0 || j >= k - 1))) ? 0.0 : tile[j][3 + c][i];
+        asm_store(pts + o, (k < P && (k == 0 || j >= k)) ? point(i, k == 0 ? 0 : k - 1, c) : point(i, j, c));
+        if (vel) asm_store(vel + o, (j == K || (k < P && (k == 0 || j >= k - 1))) ? 0.0 : tile[j][3 + c][i]);
     }
     if (tmp || sal) {
         for (int e = t; e < ns * P; e += blockDim.x) {
             const int i = e / P, j = e - i * P, k = cut[i];
             const int src = (k < P && (k == 0 || j >= k)) ? (k == 0 ? 0 : k - 1) : j;  // held value's index
             const int64_t o = row[i] * P + j;
-            if (tmp) tmp[o] = (pathline && src < K) ? tile[src][3][i] : 0.0;
-            if (sal) sal[o] = (pathline && src < K) ? tile[src][4][i] : 0.0;
+            if (tmp) asm_store(tmp + o, (pathline && src < K) ? tile[src][3][i] : 0.0);
+            if (sal) asm_store(sal + o, (pathline && src < K) ? tile[src][4][i] : 0.0);
         }
     }
     if (last) {
         for (int e = t; e < ns * 3; e += blockDim.x) {
             const int i = e / 3, c = e - i * 3, k = cut[i];
-            last[3 * row[i] + c] = (k < P) ? point(i, k == 0 ? 0 : k - 1, c) : point(i, K, c);  // line order
+            asm_store(last + 3 * row[i] + c, (k < P) ? point(i, k == 0 ? 0 : k - 1, c) : point(i, K, c));  // line order
         }
     }
 }

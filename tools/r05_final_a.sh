@@ -1,6 +1,6 @@
 # round 5, final build: GPU suite + smoke, then the profiles of the default line (config 3 Euler) and its RK4 chain
 set -o pipefail
-out=gpurun_out/r05t
+out=gpurun_out/r05w
 mkdir -p $out
 export TMPDIR=/tmp
 timeout -k 10 900 python -u -m pytest tests -m gpu -v --maxfail=5 --timeout 300 --timeout-method thread > $out/pytest.log 2>&1
