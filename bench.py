@@ -256,7 +256,8 @@ def l1_block(key, unit_s: float):
 
 def valu_block(key):
     """The VALU-issue view: how much of the SIMDs' cycles the kernel's vector instructions hold, from the same
-    profile (tools/make_traffic.py valu_issue_model: FP64 add/mul/fma 4 SIMD-cycles per wave64, other VALU 2;
+    profile (tools/make_traffic.py valu_issue_model: 4 SIMD-cycles per wave64 VALU instruction, FP64 or not, as
+    tools/fp64bench.hip measures on MI355X;
     tools/merge_issue.py valu_busy: rocprof's VALUBusy from SQ_ACTIVE_INST_VALU).  As a roofline: achieved =
     frac of the peak 1.0 (every SIMD issuing a VALU instruction every cycle)."""
     e, src = _entry_of(key)
@@ -265,8 +266,9 @@ def valu_block(key):
     return {"achieved": e["valu_issue_model"], "peak": 1.0,
             "frac": e["valu_issue_model"], "valu_busy": e.get("valu_busy"), "salu_busy": e.get("salu_busy"),
             "lds_busy": e.get("lds_busy"), "unit": "fraction of SIMD cycles",
-            "source": src + " SQ_INSTS_VALU{,_ADD_F64,_MUL_F64,_FMA_F64}: (4 x FP64 + 2 x other) / (1024 SIMDs x "
-                      "GRBM_GUI_ACTIVE / 8); valu_busy = SQ_ACTIVE_INST_VALU x 4 / 1024 / (GRBM_GUI_ACTIVE / 8)"}
+            "source": src + " SQ_INSTS_VALU x 4 SIMD-cycles (measured per wave64 VALU instruction, FP64 and int32 "
+                      "alike: tools/fp64bench.hip, profiles/r05/fp64bench) / (1024 SIMDs x GRBM_GUI_ACTIVE / 8); "
+                      "valu_busy = SQ_ACTIVE_INST_VALU x 4 / 1024 / (GRBM_GUI_ACTIVE / 8)"}
 
 
 def limiter_kind(l1: dict, valu: dict) -> str:
@@ -292,7 +294,7 @@ def limiter_text(l1: dict, valu: dict) -> str:
             return (f"texture-data return of the per-lane gathers: TD {td:.0%} busy (l1_return); VALU issue "
                     f"{vf:.0%} of SIMD cycles by instruction count, VALUBusy {vb:.0%} (valu_issue) -- DESIGN.md section 3")
         if vb > td + 0.1:
-            return (f"VALU issue: the FP64 geometry holds {vf:.0%} of SIMD cycles by instruction count "
+            return (f"VALU issue: the FP64 geometry's instructions hold {vf:.0%} of SIMD cycles by count "
                     f"(rocprof VALUBusy {vb:.0%}); TD {td:.0%} busy, DRAM far below its peak -- DESIGN.md section 3")
         return (f"TD return and VALU issue together: TD {td:.0%} busy, VALU {vf:.0%} of SIMD cycles by instruction "
                 f"count (VALUBusy {vb:.0%}); DRAM far below its peak -- DESIGN.md section 3")

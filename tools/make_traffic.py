@@ -55,10 +55,13 @@ if nt:
     if grbm > 0:
         rec["td_busy"] = (tdb / 256.0) / (grbm / 8.0)
         if nv and na and nm and nfm:
-            # VALU issue model: a wave64 FP64 add/mul/fma holds its 32-wide SIMD 4 cycles (78.6 TF = 16 FP64 FMA
-            # lanes per SIMD-cycle), any other VALU 2 (MI355X_MICROARCH.md); against 1024 SIMDs x the cycles
+            # VALU issue model: every wave64 VALU instruction holds its SIMD 4 cycles -- measured on MI355X for
+            # FP64 fma / add / mul and for 32-bit integer add / xor alike, 4.1-4.2 SIMD-cycles each at ~97%
+            # VALUBusy (tools/fp64bench.hip, profiles/r05/fp64bench/); against 1024 SIMDs x the cycles.  (Round
+            # 4's model priced non-FP64 instructions at 2 cycles, from the FP32 rate, and undercounted.)
             f64 = add + mul + fma
-            rec["valu_issue_model"] = (4.0 * f64 + 2.0 * (valu - f64)) / units / (1024.0 * grbm / units / 8.0)
+            rec["valu_issue_model"] = 4.0 * valu / units / (1024.0 * grbm / units / 8.0)
+            rec["valu_issue_model_fp64_only"] = 4.0 * f64 / units / (1024.0 * grbm / units / 8.0)
 recs = []
 if os.path.exists(dst):
     old = json.load(open(dst))
