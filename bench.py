@@ -7,12 +7,12 @@ mesh (synthetic, ~236k ocean cells, 60 levels), 1e7 particles per GPU, "layer 10
 MOPSPathline.run, tutorial/pyMOPSAPI.py:1396-1531; mops_amd/chain.py), each pair's duration from the
 snapshots' timestamps.  One bench "step" = the whole 7-day chain: per pair the seed location
 (hinted by each particle's cell after pair 0), locality order, 1440 integration steps, the line
-assembly + NaN cleanup, and -- for N > 1 -- an RCCL all-gather of the pair's record slab (every
-particle's trajectory records, with seeds and slot ids) over xGMI on a side stream, overlapped
-with the next pair.  ``--gpus N`` without a launcher starts the N ranks itself.
+assembly + NaN cleanup, and -- for N > 1 -- an RCCL gather to rank 0 of the pair's record slab
+(every particle's trajectory records, with seeds and slot ids; ``--gather records``: an all-gather)
+over xGMI on a side stream, overlapped with the next pair.  ``--gpus N`` without a launcher starts the N ranks itself.
 
 ``--config 2``: BASELINE configs[1] -- 1e6 particles/GPU, depth 800 m, dt 120 s, 1-day streamline
-(720 Euler steps), records all-gathered after every call for N > 1.
+(720 Euler steps), records gathered after every call for N > 1.
 
 ``--config 4``: BASELINE configs[3] -- oRRS18to6-class mesh (3.5M ocean cells, 80 levels), 1e7
 particles in total sharded over the ranks (strong scaling), depth 20 m, dt 120 s, 30-day pathline
@@ -75,12 +75,19 @@ def parse(argv=None):
                    help="config 2: particle parts on their own streams (ParticleSet.advance_pipelined)")
     p.add_argument("--chunks", type=int, default=6,
                    help="config 2: step chunks per part and segment (shorter launches whose tails overlap)")
-    p.add_argument("--gather", choices=["records", "checkpoint"], default="records",
-                   help="N > 1: 'records' (default, the north star's trajectory collection) = at every checkpoint "
-                        "(the end of a config-2 call, the end of each chained pair) one all-gather of every rank's "
-                        "record slab + seeds + slot ids (distributed.RecordGather), overlapped with the next call / "
-                        "pair; 'checkpoint' = only every particle's final state (position, depth, death, id) / the "
-                        "pair's continuation points")
+    p.add_argument("--gather", choices=["root", "records", "checkpoint"], default="root",
+                   help="N > 1, the trajectory collection at every checkpoint (the end of a config-2 call, the end "
+                        "of each chained pair): 'root' (default) = every rank's record slab + seeds + slot ids "
+                        "gathered to rank 0 (SURVEY 8e's Gather to rank 0: each sender over its own xGMI link), "
+                        "'records' = the same all-gathered to every rank (distributed.RecordGather mode 'all'); "
+                        "both overlapped with the next call / pair.  DESIGN.md section 7 models both: at config 3 "
+                        "and 8 ranks a ring all-gather moves 7 x 11.5 GB per rank per pair (~0.53 s against a "
+                        "0.5 s pair), the gather 11.5 GB per link (~75 ms).  'checkpoint' = only every particle's "
+                        "final state (position, depth, death, id) / the pair's continuation points")
+    p.add_argument("--deliver", choices=["host", "none"], default="host",
+                   help="config 3, N = 1: also time the chain with every pair's lines delivered to pinned host "
+                        "memory (chain.HostLineSink: a copy stream overlapped with the next pair), as the reference "
+                        "returns them to its caller -> the line's host_delivery block (value stays device-resident)")
     p.add_argument("--topography", choices=["sigma", "zlevel"], default="sigma",
                    help="config 2: synthetic vertical grid (synth.make_snapshot): 'zlevel' = MPAS-O z-levels with "
                         "partial bottom cells and zero-thickness inactive levels")
@@ -324,13 +331,17 @@ def roofline_block(kernel: str, avg_kernel_s: float, psteps_per_launch: float, B
     kind = limiter_kind(l1, valu)
     top = {"hbm": hbm, "l1_return": l1, "valu_issue": valu}[kind]
     return {
-        # the counter-chosen binding roof (limiter_kind); the HBM fraction BASELINE's metric asks for is the
-        # `hbm` view (the kernel is far below that roof: no workload here is DRAM-bound)
-        "bound": kind,
-        "achieved": top.get("achieved"),
-        "peak": top.get("peak"),
-        "unit": top.get("unit"),
-        "frac": top.get("frac"),
+        # top level = the HBM view, as BASELINE's metric defines the roofline (achieved DRAM GB/s over the 8 TB/s
+        # peak).  No workload here is DRAM-bound: the roof that binds, chosen
+        # from the counters (limiter_kind), is named separately in binding_roof / binding_frac.
+        "bound": "hbm",
+        "achieved": achieved,
+        "peak": PEAK_HBM_GBS,
+        "unit": "GB/s",
+        "frac": hbm["frac"],
+        "binding_roof": kind,
+        "binding_frac": top.get("frac"),
+        "binding_unit": top.get("unit"),
         "traffic": traffic,
         "traffic_source": src,
         "hbm": hbm,
@@ -473,11 +484,12 @@ def main():
     compute = torch.cuda.Stream(dev)
     comm = torch.cuda.Stream(dev)
     part_streams = [torch.cuda.Stream(dev) for _ in range(max(1, args.parts))]
-    gather_records = world > 1 and args.gather == "records"
+    gather_records = world > 1 and args.gather in ("records", "root")
     collector = ckpt = gathered_ckpt = None
     if world > 1 and gather_records:
-        # every call's record slab + seeds + slot ids, all-gathered on `comm` while the next call computes
-        collector = RecordGather(dist, ps, world, backend=args.backend, comm_stream=comm)
+        # every call's record slab + seeds + slot ids, gathered on `comm` while the next call computes
+        collector = RecordGather(dist, ps, world, backend=args.backend, comm_stream=comm,
+                                 mode="root" if args.gather == "root" else "all")
     elif world > 1:
         ckpt = torch.empty((6, n), dtype=torch.float64, device=dev)  # x, y, z, depth, death step, slot id
         gathered_ckpt = torch.empty((world, 6, n), dtype=torch.float64, device=dev)
@@ -645,7 +657,8 @@ def main():
                 "records": ps.K, "method": args.method, "parallelism": f"particle-shard x{world}",
                 "topography": args.topography,
                 "record_gather": record_gather_text(world, args, per="call", K=ps.K, collector=collector),
-                "record_gather_plan": collector.plan() if collector is not None else None,
+                "record_gather_plan": (collector.plan(compute_s_per_checkpoint=elapsed / args.steps)
+                                       if collector is not None else None),
             },
             "nominal_particle_steps_per_call": n_all * n_steps,
             "attempted_particle_steps_per_call": attempted_all,
@@ -672,10 +685,15 @@ def record_gather_text(world: int, args, per: str, K: int, collector=None) -> st
     if world == 1:
         return "none (one rank: its lines are assembled on the device every " + per + ")"
     be = "rccl" if args.backend == "nccl" else "gloo"
-    if args.gather == "records":
-        txt = (f"{be} all_gather at every {per} of each rank's record slab ({K} records x 48 B per particle, in slot "
-               "order) + seeds + slot ids (distributed.RecordGather): every rank holds every particle's trajectory "
-               "records, overlapped with the next " + per)
+    if args.gather in ("records", "root"):
+        if args.gather == "root":
+            txt = (f"{be} gather to rank 0 at every {per} of each rank's record slab ({K} records x 48 B per particle, "
+                   "in slot order) + seeds + slot ids (distributed.RecordGather mode 'root'): rank 0 holds every "
+                   "particle's trajectory records, overlapped with the next " + per)
+        else:
+            txt = (f"{be} all_gather at every {per} of each rank's record slab ({K} records x 48 B per particle, in "
+                   "slot order) + seeds + slot ids (distributed.RecordGather): every rank holds every particle's "
+                   "trajectory records, overlapped with the next " + per)
         if collector is not None:
             txt += f"; {collector.bytes_per_rank / max(1, collector.checkpoints) / 1e9:.3f} GB sent per rank per {per}"
             if collector.chunk < collector.shape[0]:
@@ -768,7 +786,7 @@ def main_chain(args, mesh, dev, world, rank):
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         if int(t[0].item()) != -int(t[1].item()):
             raise SystemExit("bench.py: ranks drew different particle counts")
-    gather_records = world > 1 and args.gather == "records"
+    gather_records = world > 1 and args.gather in ("records", "root")
     defer_lines = args.defer_lines and not gather_records  # (RecordGather reads the pair's slab in on_pair)
     gathered = torch.empty((world, n_pad, 3), dtype=torch.float64, device=dev) if world > 1 else None
     send = torch.zeros((n_pad, 3), dtype=torch.float64, device=dev) if world > 1 else None
@@ -788,7 +806,8 @@ def main_chain(args, mesh, dev, world, rank):
                 free, _ = torch.cuda.mem_get_info(dev)
                 budget = int(0.6 * (free - 2 * ps.records.numel() * 8))
                 collector[0] = RecordGather(dist, ps, world, backend=args.backend, comm_stream=comm,
-                                            max_bytes=max(budget, 1 << 30))
+                                            max_bytes=max(budget, 1 << 30),
+                                            mode="root" if args.gather == "root" else "all")
             collector[0].collect(ps, compute)
         elif world > 1:  # checkpoint: every rank gets the continuation points of all shards
             done = torch.cuda.Event(); done.record(compute)
@@ -857,10 +876,12 @@ def main_chain(args, mesh, dev, world, rank):
                           f"{mesh_class.lower()}_chain{args.config}_{args.method}_{args.particles}_{key_tail}")
     # the north star's integrator (and the reference caller's default, MOPSPathline.run(method="rk4"),
     # tutorial/pyMOPSAPI.py:1396) on the same chain, timed after the Euler line (N = 1; not part of value)
-    rk4 = None
-    if (world == 1 and args.method == "euler" and args.config == 3
-            and os.environ.get("MOPS_BENCH_NO_RK4") != "1"):
+    rk4 = deliver = None
+    companions = os.environ.get("MOPS_BENCH_NO_RK4") != "1" and os.environ.get("MOPS_BENCH_NO_COMPANIONS") != "1"
+    if world == 1 and args.method == "euler" and args.config == 3 and companions:
         rk4 = chain_rk4_companion(args, chain, seeds_dev, compute, n, n_pad, gaps, B, mesh_class)
+    if world == 1 and args.method == "euler" and args.config == 3 and companions and args.deliver == "host":
+        deliver = chain_host_delivery(args, chain, seeds_dev, compute, n, n_pad, gaps, elapsed / args.steps)
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         seed_cells = dmesh_locate_host(dmesh, seeds, dev)
@@ -908,7 +929,8 @@ def main_chain(args, mesh, dev, world, rank):
                                   "each pair's lines assembled before the next pair starts"),
                 "record_gather": record_gather_text(world, args, per="pair", K=max(g // args.record for g in gaps),
                                                     collector=collector[0]),
-                "record_gather_plan": collector[0].plan() if collector[0] is not None else None},
+                "record_gather_plan": (collector[0].plan(compute_s_per_checkpoint=elapsed / args.steps / args.pairs)
+                                       if collector[0] is not None else None)},
             "nominal_particle_steps_per_call": n_all * n_steps,
             "attempted_particle_steps_per_call": attempted_all / args.steps,
             "roofline": roof,
@@ -916,9 +938,57 @@ def main_chain(args, mesh, dev, world, rank):
         }
         if rk4 is not None:
             line["rk4_companion"] = rk4
+        if deliver is not None:
+            line["host_delivery"] = deliver
         print(json.dumps(line))
     if world > 1:
         dist.destroy_process_group()
+
+
+def chain_host_delivery(args, chain, seeds_dev, compute, n, n_pad, gaps, plain_s_per_chain):
+    """The caller-shaped rate: the same Euler chain with every pair's lines delivered to pinned
+    host memory, as the reference's API returns them (MOPSApp.cpp:254-337 vector<TrajectoryLine>;
+    bindings.cpp:383-455 list[dict]; MOPSPathline.run's per-pair accumulation, pyMOPSAPI.py:1497-1518).
+    chain.HostLineSink stages each pair's lines on the device and moves them over PCIe on a copy stream while
+    the next pair computes.  One untimed and one timed chain; exposed_d2h_ms_per_pair = (this chain - the
+    line's device-resident chain) / pairs."""
+    import torch
+    from mops_amd.chain import HostLineSink
+    K = max(g // args.record for g in gaps)
+    t_alloc = time.perf_counter()
+    sink = HostLineSink(n, K, compute.device)
+    alloc_s = time.perf_counter() - t_alloc
+
+    def run(timed):
+        res = chain.run(seeds_dev, depth=args.depth, method=1, delta_t=args.dt, record_t=args.record,
+                        keep_lines=False, compute_stream=compute, on_lines=sink,
+                        segment_steps=args.segment if args.segment else -1, record_stride=n_pad,
+                        compact_chunks=RK4_COMPACT_CHUNKS)
+        compute.synchronize()
+        sink.synchronize()
+        return res
+
+    run(False)
+    sink.d2h_events.clear()
+    sink.pairs = 0
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    res = run(True)
+    torch.cuda.synchronize()
+    el = time.perf_counter() - t0
+    att = float(res["attempted"].item())
+    st = sink.d2h_stats()
+    pairs = len(gaps)
+    return {"value": att / el, "unit": "particle-steps/s", "ms_per_chain": el * 1e3,
+            "exposed_d2h_ms_per_pair": (el - plain_s_per_chain) * 1e3 / pairs,
+            "d2h_bytes_per_pair": st["bytes"] / pairs, "d2h_ms_per_pair": st["ms"] / pairs, "d2h_gbs": st["gbs"],
+            "pinned_host_bytes": sum(v.numel() * v.element_size() for b in sink.hostbufs for v in b.values()),
+            "setup_s": alloc_s,
+            "note": ("the line's Euler chain with every pair's lines {points, velocity, temperature, salinity} + row "
+                     "ids delivered to pinned host buffers (chain.HostLineSink: a device staging copy on the compute "
+                     "stream, then PCIe on a copy stream overlapped with the next pair; two buffer sets, a caller "
+                     "consumes each pair before the one two pairs later arrives); value = attempted particle-steps / "
+                     "s including the last pair's copy; not part of the line's value, which keeps the lines in HBM")}
 
 
 RK4_COMPACT_CHUNKS = 6  # PathlineChain.run's default: launches per pair with a dead-particle compaction between

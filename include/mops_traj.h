@@ -271,7 +271,12 @@ int64_t mops_traj_num_steps(const mops_traj_cfg* cfg);
  * consecutive step ranges is identical to one call over [0, n_steps); a
  * caller that moves particles between slots in between (a re-sort) moves
  * every record slot, or clears the moved dead particles' unsampled slots
- * (mops_records_clear_dead). */
+ * (mops_records_clear_dead).
+ * Streams: pathline launches keep one small device flag per HIP stream in
+ * the mesh (the cooperative-tile selection), freed with the mesh.  Use
+ * long-lived streams (torch's pool, or streams created once): a stream
+ * destroyed while its launches still run, whose handle a new stream then
+ * reuses, would share that flag with the old launches. */
 mops_status mops_traj_advance(const mops_mesh* mesh, const mops_field* front, const mops_field* back,
                               const mops_traj_cfg* cfg, const mops_particles* particles,
                               int64_t step_begin, int64_t step_end, double* d_records,

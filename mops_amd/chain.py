@@ -404,6 +404,101 @@ class PathlineChain:
                 on_lines(p, {k: v[:, sl] for k, v in out.items()}, ps.ids[lo:hi])
 
 
+class HostLineSink:
+    """A ``PathlineChain.run(on_lines=...)`` writer hook that delivers every pair's lines to host memory, as
+    the reference returns them to its caller (``MOPSApp::runPathLine`` -> ``vector<TrajectoryLine>``,
+    src/Core/MOPSApp.cpp:254-337; pyMOPS -> ``list[dict]``, tools/pyMOPS/bindings.cpp:383-455;
+    ``MOPSPathline.run`` accumulates them per pair, tutorial/pyMOPSAPI.py:1497-1518).
+
+    Overlap: each chunk of lines is first copied on the compute stream into one of two device staging slabs
+    (a device-to-device copy at HBM speed), then a copy stream moves that slab into pinned host buffers while
+    the next pair computes.  Pair p uses slot p % 2 (device staging and host buffers alike); before pair p
+    writes a slot, the compute stream waits for the host copy of pair p - 2 out of it.  So a caller reads
+    pair p's host lines (``host(p)``) after ``synchronize()`` or after pair p + 1 was handed, and has until
+    pair p + 2's lines arrive to consume them (``keep_all=True`` instead keeps every pair's host copy).
+
+    ``ids[p]`` (host int32): the particle of each row (the chain hands lines in slot order)."""
+
+    def __init__(self, n: int, k_max: int, device, keep_all: bool = False):
+        import torch
+        self.torch = torch
+        self.n, self.P = int(n), int(k_max) + 1
+        self.dev = torch.device(device)
+        self.copy = torch.cuda.Stream(self.dev)
+        self.keep_all = keep_all
+        self.stage = [self._bufs(self.dev) for _ in range(2)]
+        self.hostbufs = [] if keep_all else [self._bufs("cpu") for _ in range(2)]
+        self._pinned = {}  # pair -> host buffers (keep_all)
+        self._done = [None, None]  # copy-stream event of the last host copy out of each staging slot
+        self._cur = -1
+        self.d2h_events = []  # (start, end, bytes) per chunk on the copy stream
+        self.pairs = 0
+        self._width = {}  # pair -> samples per line (the first pair's K + 1, later pairs K)
+
+    def _bufs(self, dev):
+        t = self.torch
+        pin = dict(pin_memory=True) if dev == "cpu" else {}
+        return dict(points=t.empty((self.n, self.P, 3), dtype=t.float64, device=dev, **pin),
+                    velocity=t.empty((self.n, self.P, 3), dtype=t.float64, device=dev, **pin),
+                    temperature=t.empty((self.n, self.P), dtype=t.float64, device=dev, **pin),
+                    salinity=t.empty((self.n, self.P), dtype=t.float64, device=dev, **pin),
+                    ids=t.empty((self.n,), dtype=t.int32, device=dev, **pin))
+
+    def host(self, p: int) -> dict:
+        """Pair p's lines on the host (rows in the chain's slot order, ``ids`` = each row's particle)."""
+        b = self._pinned[p] if self.keep_all else self.hostbufs[p % 2]
+        w = self._width[p]
+        return {k: (v if k == "ids" else v[:, :w]) for k, v in b.items()}
+
+    def __call__(self, p: int, lines: dict, ids):
+        torch = self.torch
+        cs = torch.cuda.current_stream(self.dev)
+        slot = p % 2
+        if p != self._cur:  # first chunk of pair p: slot p % 2's previous host copy must be done
+            self._cur, self._row = p, 0
+            if self._done[slot] is not None:
+                cs.wait_event(self._done[slot])
+            self.pairs += 1
+            if self.keep_all:
+                self._pinned[p] = self._bufs("cpu")
+        w = lines["points"].shape[1]
+        self._width[p] = w
+        lo, hi = self._row, self._row + lines["points"].shape[0]
+        self._row = hi
+        st = self.stage[slot]
+        for k, v in lines.items():  # compute stream: device staging (the chain reuses its chunk buffers next)
+            st[k][lo:hi, :w].copy_(v)
+        st["ids"][lo:hi].copy_(ids)
+        ready = torch.cuda.Event()
+        ready.record(cs)
+        self.copy.wait_event(ready)
+        dst = self._pinned[p] if self.keep_all else self.hostbufs[slot]
+        with torch.cuda.stream(self.copy):
+            e0 = torch.cuda.Event(enable_timing=True)
+            e0.record(self.copy)
+            nbytes = 0
+            for k in ("points", "velocity", "temperature", "salinity"):
+                # whole rows lo..hi of the staging slab (contiguous), the first w samples of each are the pair's
+                dst[k][lo:hi].copy_(st[k][lo:hi], non_blocking=True)
+                nbytes += st[k][lo:hi].numel() * 8
+            dst["ids"][lo:hi].copy_(st["ids"][lo:hi], non_blocking=True)
+            nbytes += (hi - lo) * 4
+            e1 = torch.cuda.Event(enable_timing=True)
+            e1.record(self.copy)
+        self.d2h_events.append((e0, e1, nbytes))
+        self._done[slot] = e1
+
+    def synchronize(self):
+        self.copy.synchronize()
+
+    def d2h_stats(self) -> dict:
+        """Bytes, milliseconds and GB/s of the host copies so far (copy-stream events; after synchronize)."""
+        ms = sum(a.elapsed_time(b) for (a, b, _) in self.d2h_events)
+        by = sum(n for (_, _, n) in self.d2h_events)
+        return {"bytes": by, "ms": ms, "gbs": by / (ms * 1e-3) / 1e9 if ms > 0 else None,
+                "chunks": len(self.d2h_events), "pairs": self.pairs}
+
+
 def cu_split_streams(device, side_cus: int):
     """(compute, side): two HIP streams that partition the device's CUs
     (hipExtStreamCreateWithCUMask), ``side_cus`` of them for the side stream.

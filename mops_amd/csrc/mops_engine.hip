@@ -2270,7 +2270,9 @@ __global__ void __launch_bounds__(256) assemble_clean_kernel(int64_t n, int K, c
     const int ns = (int)((n - s0) < kAsmSlots ? (n - s0) : kAsmSlots);
     const int P = K + 1;
 #if MOPS_ASM_V2
-    if (ns == kAsmSlots && (stride & 1) == 0) {  // (block-uniform) 16-B pieces: 2 slots per load
+    // (block-uniform) 16-B pieces, 2 slots per load: needs an even stride and a 16-B aligned slab (a caller's
+    // finalize_range passes records + 8 lo for any lo)
+    if (ns == kAsmSlots && (stride & 1) == 0 && (reinterpret_cast<uintptr_t>(rec) & 15) == 0) {
         for (int e = t; e < K * 6 * (kAsmSlots / 2); e += blockDim.x) {
             const int i2 = e % (kAsmSlots / 2), c = (e / (kAsmSlots / 2)) % 6, kk = e / ((kAsmSlots / 2) * 6);
             const double2 v = *reinterpret_cast<const double2*>(rec + kk * 6 * stride + c * stride + s0 + 2 * i2);
@@ -3525,6 +3527,8 @@ mops_status mops_mesh_create(const mops_mesh_desc* desc, void* stream, mops_mesh
         return fail(MOPS_ERR_UNSUPPORTED, "mops_mesh_create: 5 (nVertices + 1) (nVertLevels - 1) >= 2^32");
     if (C > ((int64_t)1 << 30))  // the bucket directory's 32-bit size doubles up to 2C slots
         return fail(MOPS_ERR_UNSUPPORTED, "mops_mesh_create: nCells > 2^30");
+    if (MOPS_CPOLY_RANK && maxE <= 7 && C * (int64_t)14 >= ((int64_t)1 << 32))  // d_cpolyr's 32-bit piece index
+        return fail(MOPS_ERR_UNSUPPORTED, "mops_mesh_create: 14 nCells >= 2^32 (the cell-rank polygon's 32-bit index)");
     if (!desc->h_n_edges_on_cell || !desc->h_vertices_on_cell || !desc->h_cells_on_cell || !desc->h_cell_coord ||
         !desc->h_vertex_coord)
         return fail(MOPS_ERR_INVALID, "mops_mesh_create: missing mesh array");

@@ -108,6 +108,46 @@ def all_gather_flat(dist, out, inp, backend: str, group=None):
         out.copy_(o)
 
 
+def gather_flat(dist, out, inp, backend: str, world: int, rank: int, dst: int = 0, group=None):
+    """One gather of every rank's flat slab into ``out`` ([world * inp.numel()]) on rank ``dst`` only
+    (SURVEY.md §8e's "Gather to rank 0").  nccl (RCCL) runs it as point-to-point sends over each
+    sender's direct xGMI link to the root, on the caller's current stream; gloo stages device tensors
+    through host memory.  ``out`` is ignored on the other ranks (None allowed)."""
+    import torch
+    if backend == "nccl" or not inp.is_cuda:
+        gl = list(out.view(world, -1).unbind(0)) if rank == dst else None
+        dist.gather(inp, gather_list=gl, dst=dst, group=group)
+    else:
+        gl = [torch.empty(inp.shape, dtype=inp.dtype) for _ in range(world)] if rank == dst else None
+        dist.gather(inp.cpu(), gather_list=gl, dst=dst, group=group)
+        if rank == dst:
+            out.view(world, -1).copy_(torch.stack(gl))
+
+
+# xGMI: 7 point-to-point links per MI355X, ~153 GB/s each (one process per GPU on one node)
+XGMI_LINK_GBS = 153.0
+
+
+def gather_seconds(sent_bytes: float, world: int, link_gbs: float = XGMI_LINK_GBS) -> dict:
+    """Modeled seconds of one checkpoint's exchange when every rank contributes ``sent_bytes`` (DESIGN.md
+    section 7's table).  xGMI is point-to-point, so the models differ in how many links carry the bytes:
+
+    - all_gather_ring: a single ring, every rank receives (world-1) slabs through one link;
+    - all_gather_direct: fully connected, each rank receives each peer's slab over that peer's own link, all
+      links at once (the lower bound for any all-gather);
+    - root_direct: Gather to rank 0, every sender over its own link to the root, in parallel;
+    - root_serial: the root's receives one after another (the upper bound for the gather).
+
+    Every rank's HBM takes (world-1) slabs in an all-gather, only rank 0's in a gather."""
+    w = int(world)
+    if w <= 1:
+        return {"link_gbs": link_gbs, "all_gather_ring": 0.0, "all_gather_direct": 0.0, "root_direct": 0.0,
+                "root_serial": 0.0}
+    one = float(sent_bytes) / (link_gbs * 1e9)
+    return {"link_gbs": link_gbs, "all_gather_ring": (w - 1) * one, "all_gather_direct": one, "root_direct": one,
+            "root_serial": (w - 1) * one}
+
+
 class RecordGather:
     """The north star's trajectory collection: at every checkpoint -- the end of a
     StreamLine call or of a chained pathline pair -- each rank's record slab is all-gathered, so
@@ -130,12 +170,25 @@ class RecordGather:
     ``on_chunk(gathered, k0, k1)`` (enqueued on the comm stream before the next chunk overwrites the ring)
     is where an output writer takes each chunk.
 
+    ``mode``: "all" (the default: all_gather, every rank holds every record) or "root" (Gather to rank 0:
+    only rank 0 receives, allocates the ring, calls ``on_chunk`` and can rebuild lines; every sender uses
+    its own xGMI link, DESIGN.md section 7 models both).
+
     Torch device tensors (RCCL, or gloo staged through the host) and CPU tensors (gloo tests)."""
 
+    # PathlineChain.run refuses defer_lines with an on_pair that reads the pair's record slab (ADVICE r5):
+    # collect() does, and a bound method exposes its function's attributes (set below the class)
+    reads_records = True
+
     def __init__(self, dist, ps, world: int, backend: str = "nccl", comm_stream=None, group=None,
-                 max_bytes: int | None = None, on_chunk=None):
+                 max_bytes: int | None = None, on_chunk=None, mode: str = "all"):
         import torch
+        if mode not in ("all", "root"):
+            raise ValueError("RecordGather mode: 'all' or 'root'")
         self.dist, self.world, self.backend, self.group = dist, int(world), backend, group
+        self.mode = mode
+        self.rank = dist.get_rank(group) if self.world > 1 else 0
+        self.receives = mode == "all" or self.rank == 0
         self.torch = torch
         self.shape = tuple(ps.records.shape)            # [K_max][6][stride]
         self.stride = self.shape[2]
@@ -152,8 +205,10 @@ class RecordGather:
             dist.all_reduce(t, op=dist.ReduceOp.MIN, group=group)
             self.chunk = int(t.item())
         self.on_chunk = on_chunk
-        self.gathered = torch.empty((self.world, self.chunk, 6, self.stride), dtype=torch.float64, device=dev)
-        self.gathered_aux = torch.empty((self.world, 4, self.stride), dtype=torch.float64, device=dev)
+        wr = self.world if self.receives else 0  # (root mode: the senders hold no ring)
+        self.gathered = torch.empty((wr, self.chunk, 6, self.stride), dtype=torch.float64, device=dev)
+        self.gathered_aux = torch.empty((wr, 4, self.stride), dtype=torch.float64, device=dev)
+        self.gather_events = []  # (start, end) comm-stream events of every checkpoint's exchange (CUDA)
         self._read = {}      # id(slab / aux) -> comm-stream event after the gather that read it
         self._i = 0
         self.K = 0            # records of the last gathered checkpoint
@@ -195,17 +250,23 @@ class RecordGather:
         if self.cuda:
             self.comm.wait_event(ready)
         with cctx:
-            all_gather_flat(self.dist, self.gathered_aux.view(-1), aux.view(-1), self.backend, self.group)
+            if self.cuda:
+                t0 = torch.cuda.Event(enable_timing=True)
+                t0.record(self.comm)
+            self._exchange(self.gathered_aux.view(-1), aux.view(-1))
             row = 6 * self.stride
             for k0 in range(0, K, self.chunk):
                 k1 = min(K, k0 + self.chunk)
                 m = (k1 - k0) * row
-                all_gather_flat(self.dist, self.gathered.view(-1)[: self.world * m],
-                                slab.view(-1)[k0 * row: k1 * row], self.backend, self.group)
-                if self.on_chunk is not None:
+                self._exchange(self.gathered.view(-1)[: self.world * m] if self.receives else None,
+                               slab.view(-1)[k0 * row: k1 * row])
+                if self.on_chunk is not None and self.receives:
                     self.on_chunk(self.gathered.view(-1)[: self.world * m].view(self.world, k1 - k0, 6, self.stride),
                                   k0, k1)
             if self.cuda:
+                t1 = torch.cuda.Event(enable_timing=True)
+                t1.record(self.comm)
+                self.gather_events.append((t0, t1))
                 ev = torch.cuda.Event()
                 ev.record(self.comm)
                 self._read[id(slab)] = ev
@@ -216,7 +277,17 @@ class RecordGather:
         self.bytes_per_rank += (K * 6 + 4) * self.stride * 8
         return self.done
 
-    def plan(self) -> dict:
+    def _exchange(self, out, inp):
+        if self.mode == "all":
+            all_gather_flat(self.dist, out, inp, self.backend, self.group)
+        else:
+            gather_flat(self.dist, out, inp, self.backend, self.world, self.rank, 0, self.group)
+
+    def gather_ms(self) -> list:
+        """Comm-stream milliseconds of every checkpoint's exchange so far (CUDA; call after synchronize)."""
+        return [a.elapsed_time(b) for (a, b) in self.gather_events]
+
+    def plan(self, compute_s_per_checkpoint: float | None = None) -> dict:
         """The per-rank memory plan of the collection (bench.py prints it for N > 1): bytes gathered per
         checkpoint (every rank's slab at the longest record count), the ring that receives them (the whole
         gathered slab, or chunks of records when max_bytes bounds it), the spare slab and aux buffers, and
@@ -227,7 +298,22 @@ class RecordGather:
                "sent_bytes_per_checkpoint": (self.shape[0] * 6 + 4) * self.stride * 8,
                "ring_bytes": self.gathered.numel() * 8 + self.gathered_aux.numel() * 8,
                "ring_records": self.chunk, "chunked": self.chunk < self.shape[0],
-               "spare_slab_bytes": self.spare.numel() * 8, "aux_bytes": sum(a.numel() for a in self.aux) * 8}
+               "spare_slab_bytes": self.spare.numel() * 8, "aux_bytes": sum(a.numel() for a in self.aux) * 8,
+               "mode": self.mode,
+               "received_bytes_per_checkpoint": ((self.world - 1) * (self.shape[0] * 6 + 4) * self.stride * 8
+                                                 if self.receives else 0)}
+        sent = (self.shape[0] * 6 + 4) * self.stride * 8
+        model = gather_seconds(sent, self.world)
+        out["modeled_seconds_per_checkpoint"] = model
+        if compute_s_per_checkpoint:
+            mine = model["all_gather_ring"] if self.mode == "all" else model["root_serial"]
+            out["compute_seconds_per_checkpoint"] = compute_s_per_checkpoint
+            out["modeled_gather_over_compute"] = {k: v / compute_s_per_checkpoint for k, v in model.items()
+                                                  if k != "link_gbs"}
+            out["modeled_worst_case_over_compute"] = mine / compute_s_per_checkpoint
+        if self.gather_events:
+            ms = self.gather_ms()
+            out["measured_gather_ms"] = {"mean": sum(ms) / len(ms), "max": max(ms), "checkpoints": len(ms)}
         if self.cuda:
             free, total = self.torch.cuda.mem_get_info(self.spare.device)
             out.update(hbm_free_bytes=int(free), hbm_total_bytes=int(total))
@@ -241,6 +327,8 @@ class RecordGather:
         """(records [K][6][n_total], seeds [n_total][3]) of the last checkpoint in global particle
         order (call after ``synchronize``; needs the whole slab in one chunk)."""
         K, w = self.K, self.world
+        if not self.receives:
+            raise ValueError("root mode: only rank 0 holds the gathered records")
         if K > self.chunk:
             raise ValueError("the last checkpoint was gathered in chunks (max_bytes): take them in on_chunk")
         g = self.gathered.view(-1)[: w * K * 6 * self.stride].view(w, K * 6, self.stride)
@@ -270,6 +358,9 @@ class RecordGather:
                                             C.c_void_p(sal.data_ptr()), C.c_void_p(last.data_ptr()), C.c_void_p(st)),
                 "mops_traj_finalize")
         return dict(points=pts, velocity=vel, temperature=tmp, salinity=sal, lastPoint=last)
+
+
+RecordGather.collect.reads_records = True  # (on_pair = rg.collect: a bound method reads its function's attributes)
 
 
 def _null():

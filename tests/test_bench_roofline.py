@@ -49,9 +49,10 @@ R04 = "20548e0af4c5f230"
 @pytest.mark.parametrize("key,kind", [(C3, "valu_issue"), (C4, "l1_return"), (C2, "l1_return"),
                                       ("orrs18to6_chain5_euler_12500000_seg4320", "valu_issue")])
 def test_roofline_bound_is_the_counter_chosen_limiter(key, kind, monkeypatch):
-    """The line's roofline.bound names the roof the counters show binding (bench.limiter_kind) -- VALU issue
-    for the cooperative configs 3/5 kernel, the TD return for config 4 (and config 2, where TD is the busier
-    of the two) -- and its achieved / peak / frac are that view's; the HBM fraction stays as the `hbm` view."""
+    """The line's roofline.binding_roof names the roof the counters show binding (bench.limiter_kind) -- VALU
+    issue for the cooperative configs 3/5 kernel, the TD return for config 4 (and config 2, where TD is the
+    busier of the two) -- with binding_frac that view's; the top-level bound / achieved / peak / frac are the
+    HBM view BASELINE's metric defines (a consumer reading roofline.frac gets the HBM fraction)."""
     import bench
     ents = _entries_of_build(R04)
     ents.update(_entries_of_build(bench.engine_build_id()))
@@ -64,10 +65,12 @@ def test_roofline_bound_is_the_counter_chosen_limiter(key, kind, monkeypatch):
     monkeypatch.setattr(bench, "measured_entry", lambda k: (e, "test"))
     monkeypatch.setattr(bench, "measured_traffic", lambda k: (float(e["bytes_per_unit"]), "test"))
     r = bench.roofline_block("k", 0.5, 1e10, 3660.0, key)
-    assert r["bound"] == kind
+    assert r["binding_roof"] == kind
     view = r[kind]
-    assert (r["achieved"], r["peak"], r["frac"]) == (view["achieved"], view["peak"], view["frac"])
-    assert 0.0 < r["frac"] <= 1.0
+    assert (r["binding_frac"], r["binding_unit"]) == (view["frac"], view["unit"])
+    assert 0.0 < r["binding_frac"] <= 1.0
+    assert r["bound"] == "hbm" and r["unit"] == "GB/s" and r["peak"] == bench.PEAK_HBM_GBS
+    assert (r["achieved"], r["frac"]) == (r["hbm"]["achieved"], r["hbm"]["frac"])
     assert r["hbm"]["unit"] == "GB/s" and r["hbm"]["peak"] == bench.PEAK_HBM_GBS
     assert r["hbm"]["frac"] == pytest.approx(e["bytes_per_unit"] / 0.5 / 1e9 / bench.PEAK_HBM_GBS)
     if kind == "valu_issue":

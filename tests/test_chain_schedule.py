@@ -77,7 +77,10 @@ def test_bench_default_is_config3():
     assert (a.config, a.particles, a.dt, a.pairs, a.mode, a.method) == (3, 10_000_000, 60, 7, "pathline", "euler")
     assert (a.steps, a.warmup) == (20, 5)
     a = b.apply_config_defaults(b.parse([]))
-    assert a.config == 3 and (a.steps, a.warmup) == (3, 1) and a.gather == "records"
+    # the N > 1 collection the time model favours (a ring all-gather of config 3's records
+    # is as long as the pair it overlaps; the gather to rank 0 moves one slab per link), and the caller-shaped
+    # host delivery beside the device-resident value
+    assert a.config == 3 and (a.steps, a.warmup) == (3, 1) and a.gather == "root" and a.deliver == "host"
     from mops_amd import chain
     assert chain.pair_gaps(b.chain_timestamps(3, 7)) == [86400] * 7
     a5 = b.apply_config_defaults(b.parse(["--config", "5"]))
@@ -99,7 +102,7 @@ class _Shard:
         return old
 
 
-def _gather_worker(rank, world, port, q, ring_records=1):
+def _gather_worker(rank, world, port, q, ring_records=1, mode="all"):
     import torch
     import torch.distributed as dist
     from oracle import oracle as O
@@ -134,14 +137,27 @@ def _gather_worker(rank, world, port, q, ring_records=1):
             ids = torch.as_tensor(perm.astype(np.int32))
             shard = _Shard(rec, sd, ids, K)
             if coll is None:
-                coll = RecordGather(dist, shard, world, backend="gloo")
+                coll = RecordGather(dist, shard, world, backend="gloo", mode=mode)
             coll.collect(shard)
-            got_rec, got_seeds = coll.unsharded(n_total)
-            ok &= np.array_equal(got_rec[:, 0:3].numpy().transpose(2, 0, 1), ref["rec_pos"])
-            ok &= np.array_equal(got_rec[:, 3:6].numpy().transpose(2, 0, 1), ref["rec_vel"])
-            ok &= np.array_equal(got_seeds.numpy(), s_all)
+            if coll.receives:
+                got_rec, got_seeds = coll.unsharded(n_total)
+                ok &= np.array_equal(got_rec[:, 0:3].numpy().transpose(2, 0, 1), ref["rec_pos"])
+                ok &= np.array_equal(got_rec[:, 3:6].numpy().transpose(2, 0, 1), ref["rec_vel"])
+                ok &= np.array_equal(got_seeds.numpy(), s_all)
+            else:  # root mode: the senders hold no gathered records
+                ok &= mode == "root" and rank > 0 and coll.gathered.numel() == 0
+                try:
+                    coll.unsharded(n_total)
+                    ok = False
+                except ValueError:
+                    pass
             ok &= shard.records is not rec  # the particle set moved to the spare slab
             s_all = np.ascontiguousarray(ref["rec_pos"][:, K - 1])  # continuation points
+        if mode == "root":  # (the ring / chunk checks below are the all-gather path's)
+            pl = coll.plan()
+            ok &= pl["mode"] == "root" and (pl["received_bytes_per_checkpoint"] > 0) == (rank == 0)
+            q.put((rank, bool(ok)))
+            return
         # bounded ring: the last checkpoint again, gathered in chunks of `ring_records` records through
         # on_chunk (max_bytes below one checkpoint's gathered slab: the multi-chunk path config 5 takes)
         chunks = []
@@ -174,12 +190,15 @@ def _gather_worker(rank, world, port, q, ring_records=1):
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world,ring_records", [(2, 1), (3, 3), (4, 1), (4, 3)])
-def test_record_gather_gloo_chain_shaped(world, ring_records):
+@pytest.mark.parametrize("world,ring_records,mode", [(2, 1, "all"), (3, 3, "all"), (4, 1, "all"), (4, 3, "all"),
+                                                     (8, 3, "all"), (8, 1, "root"), (3, 1, "root")])
+def test_record_gather_gloo_chain_shaped(world, ring_records, mode):
     """Two chained pairs with different record counts: each rank's slot-ordered records, gathered by
     RecordGather and unsharded by the slot ids, equal the single-process (oracle) records bit for bit.
     91 particles: uneven, padded shards at 3 and 4 ranks (config 4's strong-scaling split of a
-    non-divisible N); the bounded ring in chunks of 1 or 3 records (3: a ragged last chunk)."""
+    non-divisible N); the bounded ring in chunks of 1 or 3 records (3: a ragged last chunk).  World 8 is the
+    driver's scaling run's rank count; "root" is the Gather to rank 0 (bench.py's --gather root): rank 0's
+    unsharded records equal the oracle's, the senders hold none."""
     import multiprocessing as mp
     import socket
     from oracle import oracle as O
@@ -189,7 +208,7 @@ def test_record_gather_gloo_chain_shaped(world, ring_records):
         port = s.getsockname()[1]
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
-    procs = [ctx.Process(target=_gather_worker, args=(r, world, port, q, ring_records)) for r in range(world)]
+    procs = [ctx.Process(target=_gather_worker, args=(r, world, port, q, ring_records, mode)) for r in range(world)]
     for p in procs:
         p.start()
     for p in procs:
@@ -197,3 +216,33 @@ def test_record_gather_gloo_chain_shaped(world, ring_records):
     assert all(p.exitcode == 0 for p in procs)
     res = dict(q.get(timeout=5) for _ in range(world))
     assert res == {r: True for r in range(world)}
+
+
+def test_record_gather_collector_refuses_defer_lines():
+    """PathlineChain.run(defer_lines=True) swaps the record slab before on_pair, so an on_pair that
+    reads the pair's records is refused -- RecordGather.collect flags itself (reads_records), without the caller
+    setting the attribute."""
+    import torch
+    from mops_amd.chain import PathlineChain
+    from mops_amd.distributed import RecordGather
+    shard = _Shard(torch.zeros((2, 6, 4), dtype=torch.float64), torch.zeros((4, 3), dtype=torch.float64),
+                   torch.arange(4, dtype=torch.int32), 2)
+    rg = RecordGather(None, shard, 1, backend="gloo")
+    assert getattr(rg.collect, "reads_records", False)
+    chain = PathlineChain(None, lambda i, stream: None, 2, gap_seconds=3600)
+    with pytest.raises(ValueError, match="reads_records"):
+        chain.run(np.zeros((4, 3)), depth=100.0, defer_lines=True, on_pair=rg.collect)
+
+
+def test_gather_time_model():
+    """DESIGN.md section 7's table: a ring all-gather moves (world-1) slabs through one xGMI link, a direct
+    exchange (all-gather or Gather to rank 0) one slab per link in parallel; bench.py's config-3 slab at
+    8 ranks: 11.5 GB per pair -> 0.53 s on a ring, 75 ms direct."""
+    from mops_amd.distributed import XGMI_LINK_GBS, gather_seconds
+    S = (24 * 6 + 4) * 10_000_000 * 8.0  # config 3: 24 records + seeds/ids per particle
+    m = gather_seconds(S, 8)
+    assert m["all_gather_ring"] == pytest.approx(7 * S / (XGMI_LINK_GBS * 1e9))
+    assert m["all_gather_direct"] == m["root_direct"] == pytest.approx(S / (XGMI_LINK_GBS * 1e9))
+    assert m["root_serial"] == m["all_gather_ring"]
+    assert 0.5 < m["all_gather_ring"] < 0.6 and 0.07 < m["root_direct"] < 0.08
+    assert gather_seconds(S, 1)["all_gather_ring"] == 0.0

@@ -145,7 +145,7 @@ def _gather_worker_stream(rank, world, port, q):
         dist.destroy_process_group()
 
 
-def _gather_worker_chain(rank, world, port, q):
+def _gather_worker_chain(rank, world, port, q, mode="all"):
     import torch
     import torch.distributed as dist
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
@@ -166,11 +166,12 @@ def _gather_worker_chain(rank, world, port, q):
 
         def on_pair(p, last, ps):
             if coll[0] is None:
-                coll[0] = RecordGather(dist, ps, world, backend="gloo")
+                coll[0] = RecordGather(dist, ps, world, backend="gloo", mode=mode)
             coll[0].collect(ps, torch.cuda.current_stream())
             coll[0].synchronize()
             torch.cuda.synchronize()
-            pair_lines.append({k: v.cpu().numpy() for k, v in coll[0].lines(len(seeds), pathline=True).items()})
+            if coll[0].receives:  # (root mode: rank 0 only)
+                pair_lines.append({k: v.cpu().numpy() for k, v in coll[0].lines(len(seeds), pathline=True).items()})
 
         chain.run(seeds[lo:hi], depth=300.0, method=1, delta_t=600, record_t=3600, keep_lines=False, on_pair=on_pair,
                   record_stride=max_shard(len(seeds), world))
@@ -181,7 +182,7 @@ def _gather_worker_chain(rank, world, port, q):
         dist.destroy_process_group()
 
 
-def _spawn(target, world=2):
+def _spawn(target, world=2, *extra):
     import multiprocessing as mp
     import socket
     with socket.socket() as s:
@@ -189,7 +190,7 @@ def _spawn(target, world=2):
         port = s.getsockname()[1]
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
-    procs = [ctx.Process(target=target, args=(r, world, port, q)) for r in range(world)]
+    procs = [ctx.Process(target=target, args=(r, world, port, q) + tuple(extra)) for r in range(world)]
     for p in procs:
         p.start()
     got = q.get(timeout=240)
@@ -219,14 +220,15 @@ def test_two_rank_record_gather_rk4_compaction_matches_single_run(gpu, engine_li
             assert np.array_equal(call[k], ref[k]), k
 
 
-def test_two_rank_record_gather_chain_matches_single_run(gpu, engine_lib):
+@pytest.mark.parametrize("mode", ["all", "root"])
+def test_two_rank_record_gather_chain_matches_single_run(gpu, engine_lib, mode):
     """bench.py configs 3-5 at N > 1: every pair's record slab gathered (pairs of 6 h and 2 h from the
-    snapshots' timestamps); the gathered lines, concatenated as MOPSPathline.run does, equal the
-    single-process chain's lines bit for bit."""
+    snapshots' timestamps), all-gathered or (bench.py's default, --gather root) gathered to rank 0; the
+    gathered lines, concatenated as MOPSPathline.run does, equal the single-process chain's lines bit for bit."""
     from mops_amd import synth
     from mops_amd.chain import PathlineChain, snapshot_field_factory
     from mops_amd.engine import DeviceMesh
-    got = _spawn(_gather_worker_chain)
+    got = _spawn(_gather_worker_chain, 2, mode)
     mesh, _, seeds = _stream_case()
     snaps = [synth.make_snapshot(mesh, timestep=t, phase=0.35 * t) for t in range(len(CHAIN_TS))]
     dm = DeviceMesh.from_mesh(mesh)

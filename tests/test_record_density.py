@@ -110,6 +110,45 @@ def test_writer_hook_hands_the_chain_lines_in_chunks(ec_pair):
         chain.run(seeds, keep_lines=True, on_lines=on_lines, **kw)
 
 
+@pytest.mark.parametrize("keep_all", [True, False])
+def test_host_line_sink_delivers_the_device_lines(ec_pair, keep_all):
+    """bench.py's host_delivery: chain.HostLineSink copies every pair's lines into pinned host
+    buffers on a copy stream, overlapped with the next pair.  Scattered back by the row ids, the host lines
+    are the same doubles as the device lines of keep_lines (pair 1 without its first sample).  K = 24 with an
+    odd lines_chunk (the assembly's 16-B record reads at an odd slot offset) -- the chunks start at
+    odd slots, where the record slab's base is not 16-B aligned."""
+    import torch
+    import bench
+    from mops_amd import synth
+    from mops_amd.chain import HostLineSink, PathlineChain
+    from mops_amd.engine import DeviceField
+    mesh, dm, f0, f1, _, _ = ec_pair
+    f2 = DeviceField.from_snapshot(dm, synth.make_snapshot(mesh, timestep=2, phase=0.7))
+    fields = [f0, f1, f2]
+    depth = bench.layer_mid_depth(mesh, 10)
+    seeds = bench.make_seeds(100_002, 2)  # an even record stride: the 16-B path is eligible
+    n = len(seeds)
+    chain = PathlineChain(dm, lambda i, stream: fields[i], 3, gap_seconds=86400, own_fields=False)
+    kw = dict(depth=depth, method=1, delta_t=120, record_t=3600)
+    want = chain.run(seeds, **kw)
+    sink = HostLineSink(n, 24, "cuda", keep_all=keep_all)
+    res = chain.run(seeds, keep_lines=False, on_lines=sink, lines_chunk=33_333, **kw)
+    torch.cuda.synchronize()
+    sink.synchronize()
+    st = sink.d2h_stats()
+    assert st["pairs"] == 2 and st["chunks"] == 2 * 4 and st["bytes"] > 2 * n * 24 * 64
+    for p in (0, 1):
+        h = sink.host(p)
+        assert not h["points"].is_cuda and h["points"].is_pinned()
+        ids = h["ids"].long()
+        col = slice(0, 25) if p == 0 else slice(25, 49)
+        for k in ("points", "velocity", "temperature", "salinity"):
+            got = torch.empty_like(h[k])
+            got[ids] = h[k]
+            assert torch.equal(got, want[k][:, col].cpu()), (p, k)
+    assert torch.equal(res["lastPoint"], want["lastPoint"])
+
+
 def test_record_every_6_minutes_1e7_through_the_hook(ec_pair, oracle_lib):
     """1e7 particles, one daily pair at K = 240: the record slab alone is 1e7 x 240 x 48 B = 115 GB, and
     concatenated lines would add 154 GB; through the writer hook the lines live in 1e6-particle chunks.
