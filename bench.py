@@ -268,21 +268,37 @@ def l1_block(key, unit_s: float):
                       "TCP_TOTAL_CACHE_ACCESSES_sum x 64 B over the launch time (upper bound for scattered lanes)"}
 
 
+# SIMD cycles a wave64 VALU instruction holds, by class (tools/fp64bench.hip, profiles/r06/fp64bench/summary.txt:
+# SIMD-cycles per instruction x VALUBusy): FP64 rcp / rsq / sqrt seeds 16, FP32 transcendentals 8, every other VALU
+# instruction 4 -- FP64 add / mul / fma, compares, selects, conversions, 64-bit integer, VOP3 forms alike (VOP2
+# v_mov_b32 / v_add_u32 / v_xor_b32 / v_fma_f32 can dual-issue: 2 cycles in pairs, SQ_ACTIVE_INST_VALU2)
+VALU_CYC = 4.0
+VALU_CYC_TRANS_F64 = 16.0
+VALU_CYC_TRANS_F32 = 8.0
+
+
 def valu_block(key):
     """The VALU-issue view: how much of the SIMDs' cycles the kernel's vector instructions hold, from the same
-    profile (tools/make_traffic.py valu_issue_model: 4 SIMD-cycles per wave64 VALU instruction, FP64 or not, as
-    tools/fp64bench.hip measures on MI355X;
-    tools/merge_issue.py valu_busy: rocprof's VALUBusy from SQ_ACTIVE_INST_VALU).  As a roofline: achieved =
-    frac of the peak 1.0 (every SIMD issuing a VALU instruction every cycle)."""
+    profile.  Round 6 prices them by class (VALU_CYC*: 4 cycles, FP64 transcendental seeds 16, FP32 ones 8) with
+    the transcendental fractions of the profile's class mix; it reconciles with rocprof's VALUBusy
+    (SQ_ACTIVE_INST_VALU, tools/merge_issue.py), which counts the same cycles.  Entries without a class mix keep
+    the flat 4-cycle count (`priced` False).  As a roofline: achieved = frac of the peak 1.0 (every SIMD issuing
+    a VALU instruction every cycle)."""
     e, src = _entry_of(key)
     if not e or e.get("valu_issue_model") is None:
         return {"frac": None, "source": src}
-    return {"achieved": e["valu_issue_model"], "peak": 1.0,
-            "frac": e["valu_issue_model"], "valu_busy": e.get("valu_busy"), "salu_busy": e.get("salu_busy"),
+    flat = e["valu_issue_model"]  # 4 cycles x SQ_INSTS_VALU / (1024 SIMDs x cycles)
+    t64, t32 = e.get("valu_trans_f64_frac"), e.get("valu_trans_f32_frac")
+    priced = t64 is not None and t32 is not None
+    frac = flat * (1.0 + (VALU_CYC_TRANS_F64 / VALU_CYC - 1.0) * t64 + (VALU_CYC_TRANS_F32 / VALU_CYC - 1.0) * t32) \
+        if priced else flat
+    return {"achieved": frac, "peak": 1.0, "frac": frac, "priced": priced, "flat_4_cycle_frac": flat,
+            "valu_trans_f64_frac": t64, "valu_trans_f32_frac": t32,
+            "valu_busy": e.get("valu_busy"), "salu_busy": e.get("salu_busy"),
             "lds_busy": e.get("lds_busy"), "unit": "fraction of SIMD cycles",
-            "source": src + " SQ_INSTS_VALU x 4 SIMD-cycles (measured per wave64 VALU instruction, FP64 and int32 "
-                      "alike: tools/fp64bench.hip, profiles/r05/fp64bench) / (1024 SIMDs x GRBM_GUI_ACTIVE / 8); "
-                      "valu_busy = SQ_ACTIVE_INST_VALU x 4 / 1024 / (GRBM_GUI_ACTIVE / 8)"}
+            "source": src + " SQ_INSTS_VALU priced by class: 4 SIMD-cycles per wave64 instruction, FP64 transcendental "
+                      "16, FP32 transcendental 8 (tools/fp64bench.hip, profiles/r06/fp64bench), over 1024 SIMDs x "
+                      "GRBM_GUI_ACTIVE / 8; valu_busy = SQ_ACTIVE_INST_VALU x 4 / 1024 / (GRBM_GUI_ACTIVE / 8)"}
 
 
 def limiter_kind(l1: dict, valu: dict) -> str:

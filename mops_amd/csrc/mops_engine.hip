@@ -1477,21 +1477,28 @@ __device__ __forceinline__ bool eval_path(const Cell<MAXV>& c, int L, int V, con
 // One velocity evaluation.  A wave whose lanes all sit in hexagons (the bulk
 // of an MPAS mesh) runs the NV = 6 instantiation; any other wave the general
 // one.  Both compute the same operations in the same order.
+#ifndef MOPS_HEX_PR_COOP
+#define MOPS_HEX_PR_COOP 1  // the pathline RK4 kernel's tile evaluation has an NV = 6 instantiation
+#endif
+#ifndef MOPS_HEX_PR_PLAIN
+#define MOPS_HEX_PR_PLAIN 1  // ... and its per-lane evaluation
+#endif
 template <int MAXV, bool PATH, int GR, bool TCHK = false>
 __device__ __forceinline__ bool eval_at(bool hex, const Cell<MAXV>& c, int L, int V, const Field& f0,
                                         const Field& f1, double px, double py, double pz, double d, double alpha,
                                         int& hint0, int& hint1, double& hx, double& hy, double& hz, double& wv,
                                         bool coop = false, const double2* tile = nullptr, int th0 = 0, int th1 = 0) {
+    // (TCHK: the RK4 pathline kernels, four inlined evaluations per step -- code size; see MOPS_HEX_PR_*)
     if constexpr (MAXV == 7 && PATH) {
         if (coop) {  // wave-uniform: the tile instantiations
-            if (hex) return eval_path<MAXV, GR, 6, true, TCHK>(c, L, V, f0, f1, px, py, pz, d, alpha, hint0, hint1, hx,
+            if ((MOPS_HEX_PR_COOP || !TCHK) && hex) return eval_path<MAXV, GR, 6, true, TCHK>(c, L, V, f0, f1, px, py, pz, d, alpha, hint0, hint1, hx,
                                                                hy, hz, wv, tile, th0, th1);
             return eval_path<MAXV, GR, 0, true, TCHK>(c, L, V, f0, f1, px, py, pz, d, alpha, hint0, hint1, hx, hy, hz,
                                                       wv, tile, th0, th1);
         }
     }
     if constexpr (MAXV == 7) {
-        if (hex)
+        if ((MOPS_HEX_PR_PLAIN || !(PATH && TCHK)) && hex)
             return PATH ? eval_path<MAXV, GR, 6>(c, L, V, f0, f1, px, py, pz, d, alpha, hint0, hint1, hx, hy, hz, wv)
                         : eval_stream<MAXV, GR, 6>(c, L, V, f0, px, py, pz, d, hint0, hx, hy, hz, wv);
     }

@@ -77,3 +77,20 @@ def test_roofline_bound_is_the_counter_chosen_limiter(key, kind, monkeypatch):
         assert r["limiter"].startswith("VALU issue")
     else:
         assert "TD" in r["limiter"]
+
+
+def test_priced_valu_issue_reconciles_with_valu_busy():
+    """the VALU roof priced by instruction class (round 6, tools/fp64bench.hip: 4 SIMD-cycles per
+    wave64 VALU instruction, 16 for the FP64 rcp / rsq / sqrt seeds, 8 for FP32 transcendentals) on the round-5
+    config-3 entry and its committed class mix (profiles/r05/c3/valu_mix.txt: 23.1 FP64 and 2.7 FP32
+    transcendentals of 1152.3 VALU per wave-step).  The flat 4-cycle count read 0.860; the priced count agrees
+    with rocprof's independent VALUBusy (SQ_ACTIVE_INST_VALU) to 1%, which the flat one does not."""
+    import bench
+    e = _entries_of_build("c0f7b27a249dcf83").get(C3)
+    if e is None or e.get("valu_trans_f64_frac") is None:
+        pytest.skip("no round-5 config-3 entry with a class mix")
+    v = bench.valu_block(e)
+    assert v["priced"] and v["flat_4_cycle_frac"] == pytest.approx(0.8596, abs=1e-3)
+    assert v["frac"] == pytest.approx(v["flat_4_cycle_frac"] * (1 + 3 * 23.1 / 1152.3 + 2.7 / 1152.3), rel=1e-12)
+    assert abs(v["frac"] - e["valu_busy"]) < 0.01 < abs(v["flat_4_cycle_frac"] - e["valu_busy"])
+    assert bench.VALU_CYC_TRANS_F64 == 16.0 and bench.VALU_CYC_TRANS_F32 == 8.0 and bench.VALU_CYC == 4.0

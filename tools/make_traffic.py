@@ -62,6 +62,17 @@ if nt:
             f64 = add + mul + fma
             rec["valu_issue_model"] = 4.0 * valu / units / (1024.0 * grbm / units / 8.0)
             rec["valu_issue_model_fp64_only"] = 4.0 * f64 / units / (1024.0 * grbm / units / 8.0)
+            # round 6 class prices (tools/fp64bench.hip, profiles/r06/fp64bench): FP64 transcendental seeds (rcp / rsq /
+            # sqrt) hold the SIMD 16 cycles, FP32 ones 8, every other VALU instruction 4 -- the transcendental fractions
+            # of the VALU count come from the profile's mix/ pass (SQ_INSTS_VALU_TRANS_F64 / _F32 over SQ_INSTS_VALU)
+            mv = [float(r["Counter_Value"]) for f in glob.glob(f"{out}/mix/**/*counter_collection.csv", recursive=True)
+                  for r in csv.DictReader(open(f)) if "traj_kernel" in r["Kernel_Name"]
+                  and r["Counter_Name"] in ("SQ_INSTS_VALU",)]
+            t64, _ = total("SQ_INSTS_VALU_TRANS_F64", "mix")
+            t32, _ = total("SQ_INSTS_VALU_TRANS_F32", "mix")
+            if mv and sum(mv) > 0:
+                rec["valu_trans_f64_frac"] = t64 / sum(mv)
+                rec["valu_trans_f32_frac"] = t32 / sum(mv)
 recs = []
 if os.path.exists(dst):
     old = json.load(open(dst))

@@ -24,5 +24,9 @@ timeout -k 5 300 rocprofv3 --pmc SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_SCA SQ_ACTIV
     SQ_ACTIVE_INST_ANY SQ_WAVE_CYCLES SQ_BUSY_CYCLES GRBM_GUI_ACTIVE --kernel-include-regex traj_kernel --output-format csv \
     -d "$out/issue" -o p -- python3 bench.py --no-cpu-baseline --steps 1 --warmup 0 ${BENCH_ARGS:-} > "$out/issue.log" 2>&1 \
     || { echo "issue failed"; exit 1; }
+timeout -k 5 300 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_VALU_TRANS_F64 SQ_INSTS_VALU_TRANS_F32 SQ_INSTS_VALU_INT32 \
+    SQ_INSTS_VALU_INT64 SQ_INSTS_VALU_CVT SQ_INSTS_VALU_FMA_F32 --kernel-include-regex traj_kernel --output-format csv \
+    -d "$out/mix" -o p -- python3 bench.py --no-cpu-baseline --steps 1 --warmup 0 ${BENCH_ARGS:-} > "$out/mix.log" 2>&1 \
+    || { echo "mix failed"; exit 1; }
 # then: tools/make_traffic.py $out KEY profiles/pmc_traffic.json UNITS && tools/merge_issue.py $out/issue KEY profiles/pmc_traffic.json
 echo "profile ok"

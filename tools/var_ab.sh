@@ -13,6 +13,6 @@ for r in $(seq 1 ${ROUNDS:-2}); do
         > $out/${v}_$r.json 2> $out/${v}_$r.err || { echo "$v failed"; tail -20 $out/${v}_$r.err; exit 1; }
     python3 -c "
 import json; d=json.load(open('$out/${v}_$r.json')); r=d['roofline']
-print('%-12s ms/step %.3f value %.4e dispatch_ms %.3f' % ('$v', d['ms_per_step'], d['value'], r.get('avg_dispatch_ms') or 0))" | tee -a $out/ab.txt
+print('%-12s ms/step %.3f value %.4e dispatch_ms %.3f launch_ms %.3f' % ('$v', d['ms_per_step'], d['value'], r.get('avg_dispatch_ms') or 0, r.get('avg_launch_ms') or 0))" | tee -a $out/ab.txt
   done
 done
