@@ -30,6 +30,7 @@ from __future__ import annotations
 
 import argparse
 import json
+import socket
 import math
 import os
 import sys
@@ -373,6 +374,11 @@ def roofline_block(kernel: str, avg_kernel_s: float, psteps_per_launch: float, B
         "timed_unit": per,
         "particle_steps_per_launch": psteps_per_launch,
         "avg_launch_ms": avg_kernel_s * 1e3,
+        "bench_host": socket.gethostname(),
+        # the PMC entry's box and its rocprofv3 launch average: the counters' cycles are that box's, the rate above is
+        # this run's (box-to-box spread ~3%)
+        "pmc_host": (measured_entry(traffic_key)[0] or {}).get("profile_host"),
+        "pmc_avg_launch_ms": (measured_entry(traffic_key)[0] or {}).get("profile_avg_launch_ms"),
         "algorithmic_model": {
             "bytes_per_particle_step": B,
             "gbs": alg,

@@ -139,6 +139,12 @@ inline int rec_ints_for(int maxv) { return ((1 + 2 * maxv) + 3) / 4 * 4; }
 #ifndef MOPS_COOP_G
 #define MOPS_COOP_G 7  // groups per wave with a tile (LDS: 1520 B + an 80-B header each)
 #endif
+#ifndef MOPS_COOP_G_PR
+#define MOPS_COOP_G_PR MOPS_COOP_G  // ... in the RK4 kernel (2 waves/SIMD by VGPRs: LDS to spare)
+#endif
+#ifndef MOPS_COOP_R_PR
+#define MOPS_COOP_R_PR MOPS_COOP_R
+#endif
 constexpr int kTilePoly = 2 * 7;           // 16-B pieces: 7 packed polygon slots {x, y, z, B_j}
 constexpr int kCellNrm = 22;               // doubles per cell of mops_mesh::d_cnrm: 7 edge normals + pad
 constexpr int kTileNrm = kCellNrm / 2;     // ... as 11 pieces
@@ -723,7 +729,7 @@ __device__ __forceinline__ int nverts(const Cell<MAXV>& c) { return NV > 0 ? NV 
 
 // guards + TBBKernel::IsInMesh + Interpolator::CalcPolygonWachspress
 // (MPASOVisualizerKernels.cpp:744-770, TBBKernel.h:21-54, Interpolation.hpp:137-165)
-template <int MAXV, int NV, bool COOP = false>
+template <int MAXV, int NV, bool COOP = false, bool BAR = true>
 __device__ __forceinline__ bool weights(const Cell<MAXV>& c, int L, int V, double px, double py, double pz,
                                         double* w, const double4* tpoly = nullptr) {
     if (c.id < 0 || L <= 1 || L > kMaxLevels) return false;
@@ -789,7 +795,7 @@ __device__ __forceinline__ bool weights(const Cell<MAXV>& c, int L, int V, doubl
             }
             inside = inside & !(nx * px + ny * py + nz * pz < 0.0);  // no short circuit: straight-line code
             w[i] = tri_area(X[i], Y[i], Z[i], bx, by, bz, px, py, pz);
-            if constexpr (NV > 0) __builtin_amdgcn_sched_barrier(0);  // one slot at a time (register pressure)
+            if constexpr (NV > 0 && BAR) __builtin_amdgcn_sched_barrier(0);  // one slot at a time (register pressure)
         } else {
             w[i] = 0.0;
         }
@@ -1292,7 +1298,13 @@ struct Pair {
 #ifndef MOPS_PAIR_BARRIER
 #define MOPS_PAIR_BARRIER 1
 #endif
-template <int MAXV, int GR, int NV, bool COOP = false>
+#ifndef MOPS_SCHED_BAR_PR
+#define MOPS_SCHED_BAR_PR 1  // the tiled RK4 pathline evaluation keeps the per-slot / per-group scheduling barriers
+#endif
+#ifndef MOPS_SCHED_BAR_PE
+#define MOPS_SCHED_BAR_PE 1  // ... and the tiled Euler one
+#endif
+template <int MAXV, int GR, int NV, bool COOP = false, bool BAR = true>
 __device__ __forceinline__ void pair_sums(const Cell<MAXV>& c, const double* w, const double* __restrict__ pr, int L,
                                           int k, Pair& S, const double2* trec = nullptr) {
     MOPS_MARK(300 + NV);
@@ -1338,7 +1350,7 @@ __device__ __forceinline__ void pair_sums(const Cell<MAXV>& c, const double* w, 
             }
             // NV > 0 has no per-group branch: keep the groups apart, or the
             // scheduler puts every record in flight at once and spills
-            if constexpr ((NV > 0 || COOP) && MOPS_PAIR_BARRIER) __builtin_amdgcn_sched_barrier(0);
+            if constexpr ((NV > 0 || COOP) && MOPS_PAIR_BARRIER && BAR) __builtin_amdgcn_sched_barrier(0);
         }
     }
     MOPS_MARK(310 + NV);
@@ -1369,10 +1381,10 @@ __device__ __forceinline__ int layer_eval(const Cell<MAXV>& c, const double* w, 
         // the tile was filled, th: always this one in Euler; an RK4 stage after another stage moved
         // the hint (TCHK) gathers its records itself -- the next step regroups the wave)
         if constexpr (COOP && TCHK) {
-            if (h == th) pair_sums<MAXV, GR, NV, true>(c, w, f.pr, L, h, S, trec);
+            if (h == th) pair_sums<MAXV, GR, NV, true, MOPS_SCHED_BAR_PR>(c, w, f.pr, L, h, S, trec);
             else pair_sums<MAXV, GR, NV>(c, w, f.pr, L, h, S);
         } else {
-            pair_sums<MAXV, GR, NV, COOP>(c, w, f.pr, L, h, S, trec);
+            pair_sums<MAXV, GR, NV, COOP, (!COOP || MOPS_SCHED_BAR_PE)>(c, w, f.pr, L, h, S, trec);
         }
         bool ok;
         if (h == 1 && d > S.zm + eps) {  // above the surface (z_0 = z_{h-1} here)
@@ -1445,7 +1457,8 @@ __device__ __forceinline__ bool eval_path(const Cell<MAXV>& c, int L, int V, con
                                           int& hint1, double& hx, double& hy, double& hz, double& wv,
                                           const double2* tile = nullptr, int th0 = 0, int th1 = 0) {
     double w[MAXV];
-    if (!weights<MAXV, NV, COOP>(c, L, V, px, py, pz, w, reinterpret_cast<const double4*>(tile))) return false;
+    constexpr bool kBar = !COOP || (TCHK ? MOPS_SCHED_BAR_PR : MOPS_SCHED_BAR_PE);
+    if (!weights<MAXV, NV, COOP, kBar>(c, L, V, px, py, pz, w, reinterpret_cast<const double4*>(tile))) return false;
     const bool wfin = weights_finite<MAXV, NV>(c, w);
     Pair F, B;
     const int lf = layer_eval<MAXV, true, GR, MOPS_HEX_PAIRS_P ? NV : 0, COOP, TCHK>(
@@ -1562,6 +1575,15 @@ struct TrajArgs {
 #endif
 #ifndef MOPS_RK4_ACC
 #define MOPS_RK4_ACC 1  // RK4 stage velocities accumulated as they come (see traj_kernel)
+#endif
+#ifndef MOPS_RK4_FENCE
+#define MOPS_RK4_FENCE 0  // a compiler memory barrier between RK4 stages: each stage re-reads the cell's polygon,
+                          // normals and tile records instead of keeping stage 1's loads live across the step
+#endif
+#if MOPS_RK4_FENCE
+#define MOPS_STAGE_FENCE() asm volatile("" ::: "memory")
+#else
+#define MOPS_STAGE_FENCE() do { } while (0)
 #endif
 #ifndef MOPS_GR_E
 #define MOPS_GR_E 1  // level-pair records in flight per round trip, Euler
@@ -1693,7 +1715,10 @@ __global__ void __launch_bounds__(kTrajBlock, (TrajWaves<MAXV, PATH, EULER, COOP
     constexpr bool kNbrT = MOPS_NBR_TEST && MAXV == 7 && (EULER || MOPS_NBR_RK4);  // dev::nbr_stay before a walk
     // per-lane edge normals (Cell::nrm); in the cooperative kernel the same LDS holds either them (a wave in
     // lane-normal mode, c.lds_n) or the wave's tile
-    constexpr int kNrmD = 3 * kNrmSlots(MAXV) * kTrajBlock, kTileD = 2 * MOPS_COOP_G * kTilePieces;
+    // groups per tile and tile pieces per live lane at most (per kernel: the RK4 one has LDS to spare)
+    constexpr int kG = EULER ? MOPS_COOP_G : MOPS_COOP_G_PR, kR = EULER ? MOPS_COOP_R : MOPS_COOP_R_PR;
+    static_assert(kG <= 254, "group index in tkey's low byte (0xff = no tile)");
+    constexpr int kNrmD = 3 * kNrmSlots(MAXV) * kTrajBlock, kTileD = 2 * kG * kTilePieces;
     __shared__ __attribute__((aligned(16))) double s_nrm[kNrm ? (kCoop && kTileD > kNrmD ? kTileD : kNrmD) : 1];
     c.nrm = s_nrm + threadIdx.x;
     c.lds_n = kNrm && !kCoop;  // (the cooperative kernel starts in tile mode)
@@ -1703,7 +1728,7 @@ __global__ void __launch_bounds__(kTrajBlock, (TrajWaves<MAXV, PATH, EULER, COOP
     c.pr2 = s_pr2 + threadIdx.x;
     c.rb2 = s_rb2 + (kPairT && MOPS_LDS_COMPACT ? threadIdx.x : 0);
     double2* s_tile = reinterpret_cast<double2*>(s_nrm);
-    __shared__ uint4 s_hdr[kCoop ? MOPS_COOP_G * (kTileHdr / 4) : 1];
+    __shared__ uint4 s_hdr[kCoop ? kG * (kTileHdr / 4) : 1];
     const int C = a.C;
     // next recording step (the smallest j >= step_begin with (j+1) % rec_period == 0) and its
     // record index, advanced by counting instead of a 64-bit modulo per step
@@ -1818,7 +1843,7 @@ __global__ void __launch_bounds__(kTrajBlock, (TrajWaves<MAXV, PATH, EULER, COOP
                 uint64_t rem = act;
                 int g = 0, G = 0;
                 bool lead = false;
-                while (rem != 0ull && G < MOPS_COOP_G) {
+                while (rem != 0ull && G < kG) {
                     const int ld = __builtin_ctzll(rem);
                     const int kc = __builtin_amdgcn_readlane(cell, ld);
                     const int k0 = __builtin_amdgcn_readlane(hint0, ld);
@@ -1833,7 +1858,7 @@ __global__ void __launch_bounds__(kTrajBlock, (TrajWaves<MAXV, PATH, EULER, COOP
                 // the pieces are spread over the live lanes only (a dead or finished lane has left the
                 // loop): at most MOPS_COOP_R per lane
                 const int nact = __popcll(act);
-                coop = rem == 0ull && G * kTilePieces <= MOPS_COOP_R * nact;
+                coop = rem == 0ull && G * kTilePieces <= kR * nact;
     #if defined(MOPS_PROF)
                 // [6] cooperative wave-steps, [7] groups of the waves that were grouped in full (rem == 0);
                 // [8] / [9] distinct cells / distinct (cell, hint0, hint1) per wave-step (unbounded),
@@ -1889,7 +1914,7 @@ __global__ void __launch_bounds__(kTrajBlock, (TrajWaves<MAXV, PATH, EULER, COOP
                     const int rank = (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(act >> 32),
                                                                     __builtin_amdgcn_mbcnt_lo((uint32_t)act, 0u));
     #pragma unroll
-                    for (int rr = 0; rr < MOPS_COOP_R; ++rr) {
+                    for (int rr = 0; rr < kR; ++rr) {
                         const int i = rank + nact * rr;
                         if (i < np) {  // piece pc of group gg: polygon, normals, front records, back records
                             const int gg = i / kTilePieces, pc = i - gg * kTilePieces;
@@ -1981,17 +2006,20 @@ __global__ void __launch_bounds__(kTrajBlock, (TrajWaves<MAXV, PATH, EULER, COOP
             hx = sx; hy = sy; hz = sz; wv = sw;
             dev::advect((unsigned)step, x, y, z, sx, sy, sz, dt * 0.5, qx, qy, qz);
             const double a2 = PATH ? dev::dclamp(a1 + 0.5 * a.dalpha, 0.0, 1.0) : 0.0;
+            MOPS_STAGE_FENCE();
             ok = dev::eval_at<MAXV, PATH, GR, true>(hex, c, a.L, a.V, a.f0, a.f1, qx, qy, qz, d, a2, hint0, hint1, sx, sy,
                                                    sz, sw, coop, tile, th0, th1);
             if (!ok) { died = (int)step; break; }
             hx = hx + sx * 2.0; hy = hy + sy * 2.0; hz = hz + sz * 2.0; wv = wv + 2.0 * sw;
             dev::advect((unsigned)step, x, y, z, sx, sy, sz, dt * 0.5, qx, qy, qz);
+            MOPS_STAGE_FENCE();
             ok = dev::eval_at<MAXV, PATH, GR, true>(hex, c, a.L, a.V, a.f0, a.f1, qx, qy, qz, d, a2, hint0, hint1, sx, sy,
                                                    sz, sw, coop, tile, th0, th1);
             if (!ok) { died = (int)step; break; }
             hx = hx + sx * 2.0; hy = hy + sy * 2.0; hz = hz + sz * 2.0; wv = wv + 2.0 * sw;
             dev::advect((unsigned)step, x, y, z, sx, sy, sz, dt, qx, qy, qz);
             const double a4 = PATH ? dev::dclamp(a1 + a.dalpha, 0.0, 1.0) : 0.0;
+            MOPS_STAGE_FENCE();
             ok = dev::eval_at<MAXV, PATH, GR, true>(hex, c, a.L, a.V, a.f0, a.f1, qx, qy, qz, d, a4, hint0, hint1, sx, sy,
                                                    sz, sw, coop, tile, th0, th1);
             if (!ok) { died = (int)step; break; }

@@ -73,6 +73,15 @@ if nt:
             if mv and sum(mv) > 0:
                 rec["valu_trans_f64_frac"] = t64 / sum(mv)
                 rec["valu_trans_f32_frac"] = t32 / sum(mv)
+# the profiled box and the rocprofv3 kernel-trace average of the kernel that ran (stats pass), so the bench line
+# can state which box its PMC cycles came from next to its own launch time
+if os.path.exists(f"{out}/host.txt"):
+    rec["profile_host"] = open(f"{out}/host.txt").read().strip()
+st = [r for f in glob.glob(f"{out}/stats/*kernel_stats.csv") for r in csv.DictReader(open(f)) if "traj_kernel" in r["Name"]]
+if st:
+    ran = max(st, key=lambda r: float(r["AverageNs"]))
+    rec["profile_kernel"] = ran["Name"]
+    rec["profile_avg_launch_ms"] = float(ran["AverageNs"]) / 1e6
 recs = []
 if os.path.exists(dst):
     old = json.load(open(dst))

@@ -26,18 +26,6 @@ rk4ab)  # code-size variants of the tiled RK4 kernel (tools/build_variant.sh noh
   BENCH_ARGS="--method rk4 --steps 1 --warmup 1" OUT=$O/rk4ab ROUNDS=2 bash tools/var_ab.sh base ${RK4_VARIANTS:-nohexprc nohexpr} || exit 11
   cat $O/rk4ab/ab.txt
   ;;
-pcsamp)  # PC sampling of the config-3 Euler and RK4 launches (2e6 particles, one pair): hot instructions
-  export MOPS_BENCH_NO_COMPANIONS=1
-  for m in euler rk4; do
-    rm -rf /tmp/pcs_$m
-    timeout -s KILL 400 rocprofv3 --pc-sampling-beta-enabled 1 --pc-sampling-method ${PCS_METHOD:-stochastic} \
-        --pc-sampling-unit ${PCS_UNIT:-cycles} --pc-sampling-interval ${PCS_INTERVAL:-65536} -d /tmp/pcs_$m -o p \
-        --output-format csv -- python3 bench.py --no-cpu-baseline --steps 1 --warmup 0 --pairs 1 --particles 2000000 \
-        --method $m > $O/pcs_$m.log 2>&1 || { tail -20 $O/pcs_$m.log; exit 9; }
-    python3 tools/pcsamp_summary.py /tmp/pcs_$m $O/pcs_$m.txt traj_kernel || exit 10
-    du -sh /tmp/pcs_$m
-  done
-  ;;
 gputests)
   timeout -k 10 1000 python -u -m pytest tests -m gpu -v --maxfail=5 --timeout 300 --timeout-method thread > $O/pytest.log 2>&1
   rc=$?; tail -5 $O/pytest.log; [ $rc -eq 0 ] || exit 6
