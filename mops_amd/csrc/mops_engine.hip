@@ -134,10 +134,17 @@ inline int rec_ints_for(int maxv) { return ((1 + 2 * maxv) + 3) / 4 * 4; }
 #define MOPS_GR_COOP 2  // level-pair records per LDS round trip in the tile instantiations (1: +1%, 3: +7%)
 #endif
 #ifndef MOPS_COOP_R
-#define MOPS_COOP_R 12  // tile pieces per live lane at most (fewer live lanes: the lanes gather themselves)
+#define MOPS_COOP_R 13  // tile pieces per live lane at most (fewer live lanes: the lanes gather themselves)
 #endif
 #ifndef MOPS_COOP_G
-#define MOPS_COOP_G 7  // groups per wave with a tile (LDS: 1520 B + an 80-B header each)
+// groups per wave with a tile (LDS: 1296 B (6 tile slots) + an 80-B header each).  Round 6: with 7 tile slots,
+// 8 groups (12.8 KB per block) still allow the 12 blocks per CU the kernel's 168 VGPRs allow and cut the wave-steps
+// that fall back to per-lane gathers from 18.6% to 6.9%: config-3 launch 501.0 -> 491.4 ms; 9 groups (11 blocks)
+// 541 ms; 6 tile slots and 9 groups (12.4 KB) a further -0.9% (profiles/r06/ab/coop_groups_euler.txt)
+#define MOPS_COOP_G 9
+#endif
+#ifndef MOPS_COOP_RETRY
+#define MOPS_COOP_RETRY 64  // steps between regroup attempts of a wave in lane-normal mode (a power of two)
 #endif
 #ifndef MOPS_COOP_G_PR
 #define MOPS_COOP_G_PR MOPS_COOP_G  // ... in the RK4 kernel (2 waves/SIMD by VGPRs: LDS to spare)
@@ -145,12 +152,19 @@ inline int rec_ints_for(int maxv) { return ((1 + 2 * maxv) + 3) / 4 * 4; }
 #ifndef MOPS_COOP_R_PR
 #define MOPS_COOP_R_PR MOPS_COOP_R
 #endif
-constexpr int kTilePoly = 2 * 7;           // 16-B pieces: 7 packed polygon slots {x, y, z, B_j}
+#ifndef MOPS_TILE_SLOTS
+#define MOPS_TILE_SLOTS 6  // polygon slots per tile group; 6: a wave with a heptagon lane gathers per lane, the
+                           // others take 81 instead of 95 pieces per group (more groups in the same LDS)
+#endif
+static_assert(MOPS_TILE_SLOTS == 6 || MOPS_TILE_SLOTS == 7, "tile slots");
+constexpr int kTileSlots = MOPS_TILE_SLOTS;
+constexpr int kTilePoly = 2 * kTileSlots;  // 16-B pieces: the packed polygon slots {x, y, z, B_j}
 constexpr int kCellNrm = 22;               // doubles per cell of mops_mesh::d_cnrm: 7 edge normals + pad
-constexpr int kTileNrm = kCellNrm / 2;     // ... as 11 pieces
-constexpr int kTileRec = (kPairRec / 2) * 7;  // 7 level-pair records of one field
+constexpr int kCellNrmPieces = kCellNrm / 2;  // ... as 11 pieces
+constexpr int kTileNrm = (3 * kTileSlots + 1) / 2;  // the tile's normal pieces (7 slots: 11, 6 slots: 9)
+constexpr int kTileRec = (kPairRec / 2) * kTileSlots;  // the slots' level-pair records of one field
 constexpr int kTileOffNrm = kTilePoly, kTileOffRec = kTilePoly + kTileNrm;
-constexpr int kTilePieces = kTilePoly + kTileNrm + 2 * kTileRec;  // 95 pieces = 1520 B per group
+constexpr int kTilePieces = kTilePoly + kTileNrm + 2 * kTileRec;  // 95 pieces = 1520 B per group (6 slots: 81)
 constexpr int kTileHdr = 20;               // ints per group header: cell, nv, pad x2, front / back record index x 8
 // Neighbour table (maxEdges <= 7 meshes, mops_mesh::d_nbr): per cell 112 B = 7 x 16 B -- the centre as three
 // doubles, the 7 neighbour offsets q_k - c as floats, then the bitmask of the neighbours the walk considers.
@@ -497,6 +511,28 @@ __device__ __forceinline__ double tri_area(double ax, double ay, double az, doub
     return xsqrt(px * px + py * py + pz * pz) / 2.0;
 }
 
+// Wachspress without the two halvings (round 6, MOPS_WACH_X4): the reference's w_i = B_i / (A_i A_{i+1}) with
+// A = R / 2, R = sqrt(|cross|^2).  Halving is exact here, and so is scaling a product by 1/4 before rounding: with
+// mesh vertices at Earth radius (< 2^23 m) every edge difference is a multiple of 2^-30, every cross-product
+// component a multiple of 2^-60, so R is 0 or >= 2^-60 and R_i R_{i+1} is 0 or >= 2^-120 -- far from the
+// subnormal range, and far below overflow.  So fl(A_i A_{i+1}) = fl(R_i R_{i+1}) / 4 and fl(B_i / fl(A_i A_{i+1})) = fl(4 B_i / fl(R_i R_{i+1}))
+// with 4 B_i exact: the same double, inf (R = 0) and NaN included, from 4 B_i stored per cell (cell_poly_kernel,
+// load_cell) and R_i = tri_area_x2: 6 FP64 multiplies fewer per evaluation.
+#ifndef MOPS_WACH_X4
+#define MOPS_WACH_X4 1
+#endif
+__device__ __forceinline__ double tri_area_x2(double ax, double ay, double az, double bx, double by, double bz,
+                                              double cx, double cy, double cz) {
+    const double e1x = bx - ax, e1y = by - ay, e1z = bz - az;
+    const double e2x = cx - ax, e2y = cy - ay, e2z = cz - az;
+    const double px = e1y * e2z - e1z * e2y;
+    const double py = e1z * e2x - e1x * e2z;
+    const double pz = e1x * e2y - e1y * e2x;
+    return xsqrt(px * px + py * py + pz * pz);
+}
+// the per-cell Wachspress numerator as the weights read it: B_i, or 4 B_i (exact) with MOPS_WACH_X4
+__device__ __forceinline__ double wach_numerator(double B) { return MOPS_WACH_X4 ? 4.0 * B : B; }
+
 // TBBKernel::CalcPositionAfterRotation (TBBKernel.h:177-206)
 __device__ __forceinline__ void rotate(unsigned salt, double px, double py, double pz, double ax, double ay, double az, double th,
                                        double& rx, double& ry, double& rz) {
@@ -697,7 +733,7 @@ __device__ __forceinline__ void load_cell(Cell<MAXV>& c, int cell, const int* __
                     const double nx = wrap ? px[0] : px[(i + 1) % MAXV];
                     const double ny = wrap ? py[0] : py[(i + 1) % MAXV];
                     const double nz = wrap ? pz[0] : pz[(i + 1) % MAXV];
-                    c.B[i] = tri_area(qx, qy, qz, px[i], py[i], pz[i], nx, ny, nz);
+                    c.B[i] = wach_numerator(tri_area(qx, qy, qz, px[i], py[i], pz[i], nx, ny, nz));
                 } else {
                     c.B[i] = 0.0;
                 }
@@ -794,7 +830,8 @@ __device__ __forceinline__ bool weights(const Cell<MAXV>& c, int L, int V, doubl
                 nz = X[i] * by - Y[i] * bx;
             }
             inside = inside & !(nx * px + ny * py + nz * pz < 0.0);  // no short circuit: straight-line code
-            w[i] = tri_area(X[i], Y[i], Z[i], bx, by, bz, px, py, pz);
+            w[i] = MOPS_WACH_X4 ? tri_area_x2(X[i], Y[i], Z[i], bx, by, bz, px, py, pz)
+                                : tri_area(X[i], Y[i], Z[i], bx, by, bz, px, py, pz);
             if constexpr (NV > 0 && BAR) __builtin_amdgcn_sched_barrier(0);  // one slot at a time (register pressure)
         } else {
             w[i] = 0.0;
@@ -1835,7 +1872,8 @@ __global__ void __launch_bounds__(kTrajBlock, (TrajWaves<MAXV, PATH, EULER, COOP
             const bool moved = (cell != tcell) | (hk != (tkey & ~0xff));
             // tile mode: regroup when a lane moved; lane-normal mode (a wave with too many groups): try
             // again every 64 steps
-            const bool regroup = c.lds_n ? ((step - a.step_begin) & 63) == 0 : (__ballot(moved) != 0ull || !have_tile);
+            const bool regroup = c.lds_n ? ((step - a.step_begin) & (MOPS_COOP_RETRY - 1)) == 0
+                                         : (__ballot(moved) != 0ull || !have_tile);
             if (regroup) {
                 // groups of live lanes with equal (cell, hint0, hint1), found leader by leader with
                 // scalar readlanes + ballots; more than MOPS_COOP_G groups: the lanes gather themselves
@@ -1858,7 +1896,8 @@ __global__ void __launch_bounds__(kTrajBlock, (TrajWaves<MAXV, PATH, EULER, COOP
                 // the pieces are spread over the live lanes only (a dead or finished lane has left the
                 // loop): at most MOPS_COOP_R per lane
                 const int nact = __popcll(act);
-                coop = rem == 0ull && G * kTilePieces <= kR * nact;
+                coop = rem == 0ull && G * kTilePieces <= kR * nact &&
+                       (kTileSlots >= MAXV || __ballot(c.nv > kTileSlots) == 0ull);
     #if defined(MOPS_PROF)
                 // [6] cooperative wave-steps, [7] groups of the waves that were grouped in full (rem == 0);
                 // [8] / [9] distinct cells / distinct (cell, hint0, hint1) per wave-step (unbounded),
@@ -1926,7 +1965,7 @@ __global__ void __launch_bounds__(kTrajBlock, (TrajWaves<MAXV, PATH, EULER, COOP
                             const uint32_t ri = hdi[gg * kTileHdr + 4 + (f1 ? 8 : 0) + v];
                             const double2* base = isp ? cpoly2 : (isn ? cnrm2 : (f1 ? pr1 : pr0));
                             const uint64_t idx = isp ? ((uint64_t)cl * MAXV + (uint32_t)(pc >> 1)) * 2 + (uint32_t)(pc & 1)
-                                                     : (isn ? (uint64_t)cl * kTileNrm + (uint32_t)(pc - kTileOffNrm)
+                                                     : (isn ? (uint64_t)cl * kCellNrmPieces + (uint32_t)(pc - kTileOffNrm)
                                                             : (uint64_t)(ri + (uint32_t)q * pr_qstride((uint32_t)a.V)));
                             s_tile[i] = base[idx];
                         }
@@ -2990,7 +3029,7 @@ __global__ void cell_poly_kernel(int64_t C, const int* cellrec, const double4* v
             const double nx = wrap ? x[0] : x[(i + 1) % MAXV];
             const double ny = wrap ? y[0] : y[(i + 1) % MAXV];
             const double nz = wrap ? z[0] : z[(i + 1) % MAXV];
-            o = make_double4(qx, qy, qz, dev::tri_area(qx, qy, qz, x[i], y[i], z[i], nx, ny, nz));
+            o = make_double4(qx, qy, qz, dev::wach_numerator(dev::tri_area(qx, qy, qz, x[i], y[i], z[i], nx, ny, nz)));
         }
         cpoly[c * MAXV + i] = o;
         if (cnrm && 3 * i + 2 < kCellNrm) {

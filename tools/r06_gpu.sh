@@ -22,8 +22,20 @@ newtests)  # the round's new GPU tests (host delivery, root gather)
       > $O/newtests.log 2>&1
   rc=$?; tail -15 $O/newtests.log; [ $rc -eq 0 ] || exit 5
   ;;
+eulerab)  # tiled Euler kernel variants on the driver's default workload (config 3, 7-pair chain)
+  MOPS_BENCH_NO_COMPANIONS=1 BENCH_ARGS="--steps 2 --warmup 1" OUT=$O/eulerab ROUNDS=${ROUNDS:-2} bash tools/var_ab.sh base ${EULER_VARIANTS} || exit 12
+  cat $O/eulerab/ab.txt
+  ;;
+prof)  # event counters (-DMOPS_PROF builds): cooperative wave-steps, regroups, walks per variant
+  for v in ${PROF_VARIANTS:-prof7 prof8}; do
+    MOPS_TRAJ_LIB=$PWD/build/variants/libmops_$v.so MOPS_PROF_SECTIONS=1 MOPS_BENCH_NO_COMPANIONS=1 timeout -k 10 300 \
+        python3 -u bench.py --no-cpu-baseline --steps 1 --warmup 0 ${BENCH_ARGS:-} > $O/prof_$v.json 2> $O/prof_$v.err \
+        || { tail -20 $O/prof_$v.err; exit 13; }
+    grep "prof counters" $O/prof_$v.err | sed "s/^/$v: /"
+  done
+  ;;
 rk4ab)  # code-size variants of the tiled RK4 kernel (tools/build_variant.sh nohexprc / nohexpr)
-  BENCH_ARGS="--method rk4 --steps 1 --warmup 1" OUT=$O/rk4ab ROUNDS=2 bash tools/var_ab.sh base ${RK4_VARIANTS:-nohexprc nohexpr} || exit 11
+  BENCH_ARGS="--method rk4 --steps 1 --warmup 1" OUT=$O/rk4ab ROUNDS=${ROUNDS:-2} bash tools/var_ab.sh base ${RK4_VARIANTS:-nohexprc nohexpr} || exit 11
   cat $O/rk4ab/ab.txt
   ;;
 gputests)
