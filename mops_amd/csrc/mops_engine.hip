@@ -163,8 +163,13 @@ constexpr int kCellNrm = 22;               // doubles per cell of mops_mesh::d_c
 constexpr int kCellNrmPieces = kCellNrm / 2;  // ... as 11 pieces
 constexpr int kTileNrm = (3 * kTileSlots + 1) / 2;  // the tile's normal pieces (7 slots: 11, 6 slots: 9)
 constexpr int kTileRec = (kPairRec / 2) * kTileSlots;  // the slots' level-pair records of one field
-constexpr int kTileOffNrm = kTilePoly, kTileOffRec = kTilePoly + kTileNrm;
-constexpr int kTilePieces = kTilePoly + kTileNrm + 2 * kTileRec;  // 95 pieces = 1520 B per group (6 slots: 81)
+#ifndef MOPS_TILE_E1
+#define MOPS_TILE_E1 0  // the tile also holds each slot's edge vector X_{i+1} - X_i (mops_mesh::d_cedge): the
+                        // Wachspress areas skip its 3 subtractions per slot (the same doubles, computed once per cell)
+#endif
+constexpr int kTileE1 = MOPS_TILE_E1 ? kTileNrm : 0;  // edge-vector pieces (laid out like the normals)
+constexpr int kTileOffNrm = kTilePoly, kTileOffE1 = kTilePoly + kTileNrm, kTileOffRec = kTileOffE1 + kTileE1;
+constexpr int kTilePieces = kTilePoly + kTileNrm + kTileE1 + 2 * kTileRec;  // 95 pieces = 1520 B per group (6 slots: 81)
 constexpr int kTileHdr = 20;               // ints per group header: cell, nv, pad x2, front / back record index x 8
 // Neighbour table (maxEdges <= 7 meshes, mops_mesh::d_nbr): per cell 112 B = 7 x 16 B -- the centre as three
 // doubles, the 7 neighbour offsets q_k - c as floats, then the bitmask of the neighbours the walk considers.
@@ -209,6 +214,7 @@ struct mops_mesh {
     // slot j = {poly[j-1] (poly[-1] = poly[nv-1]), B_j = area(poly[j-1], poly[j], poly[j+1])}, zeros past nv
     double4* d_cpoly = nullptr;
     double* d_cnrm = nullptr;    // [C][kCellNrm] IsInMesh edge normals of the rotated polygon slots (maxv 7 meshes)
+    double* d_cedge = nullptr;   // [C][kCellNrm] edge vectors X_{i+1} - X_i of the same slots (MOPS_TILE_E1)
     uint4* d_nbr = nullptr;      // [C][kNbrQ] neighbour table (cell_nbr_kernel, dev::nbr_stay; maxv 7 meshes)
     double* d_rloc2 = nullptr;       // [C] squared hinted-locate radius (locate_radius_kernel)
     double* d_ring = nullptr;        // [C] hinted-locate ring distance (locate_radius_kernel)
@@ -530,6 +536,15 @@ __device__ __forceinline__ double tri_area_x2(double ax, double ay, double az, d
     const double pz = e1x * e2y - e1y * e2x;
     return xsqrt(px * px + py * py + pz * pz);
 }
+// ... with the edge vector e1 = b - a given (the same doubles: MOPS_TILE_E1 stores b - a per cell)
+__device__ __forceinline__ double tri_area_x2_e(double ax, double ay, double az, double e1x, double e1y, double e1z,
+                                                double cx, double cy, double cz) {
+    const double e2x = cx - ax, e2y = cy - ay, e2z = cz - az;
+    const double px = e1y * e2z - e1z * e2y;
+    const double py = e1z * e2x - e1x * e2z;
+    const double pz = e1x * e2y - e1y * e2x;
+    return xsqrt(px * px + py * py + pz * pz);
+}
 // the per-cell Wachspress numerator as the weights read it: B_i, or 4 B_i (exact) with MOPS_WACH_X4
 __device__ __forceinline__ double wach_numerator(double B) { return MOPS_WACH_X4 ? 4.0 * B : B; }
 
@@ -830,8 +845,13 @@ __device__ __forceinline__ bool weights(const Cell<MAXV>& c, int L, int V, doubl
                 nz = X[i] * by - Y[i] * bx;
             }
             inside = inside & !(nx * px + ny * py + nz * pz < 0.0);  // no short circuit: straight-line code
-            w[i] = MOPS_WACH_X4 ? tri_area_x2(X[i], Y[i], Z[i], bx, by, bz, px, py, pz)
-                                : tri_area(X[i], Y[i], Z[i], bx, by, bz, px, py, pz);
+            if constexpr (COOP && MOPS_TILE_E1 && MOPS_WACH_X4) {  // the tile's b - a of this slot
+                const double* te = reinterpret_cast<const double*>(tpoly) + 2 * kTileOffE1;
+                w[i] = tri_area_x2_e(X[i], Y[i], Z[i], te[3 * i], te[3 * i + 1], te[3 * i + 2], px, py, pz);
+            } else {
+                w[i] = MOPS_WACH_X4 ? tri_area_x2(X[i], Y[i], Z[i], bx, by, bz, px, py, pz)
+                                    : tri_area(X[i], Y[i], Z[i], bx, by, bz, px, py, pz);
+            }
             if constexpr (NV > 0 && BAR) __builtin_amdgcn_sched_barrier(0);  // one slot at a time (register pressure)
         } else {
             w[i] = 0.0;
@@ -1573,6 +1593,7 @@ struct TrajArgs {
     const int* __restrict__ n_live;  // device count of leading live slots (compaction), NULL = all n
     const double4* __restrict__ cpoly;  // per-cell rotated polygon + Wachspress B_i (mops_mesh::d_cpoly)
     const double* __restrict__ cnrm;    // per-cell edge normals (mops_mesh::d_cnrm; NULL past maxEdges 7)
+    const double* __restrict__ cedge;   // per-cell edge vectors (mops_mesh::d_cedge; MOPS_TILE_E1 only)
     const uint4* __restrict__ nbr;      // per-cell neighbour table (mops_mesh::d_nbr; NULL past maxEdges 7)
     const double2* __restrict__ cpolyr;  // mops_mesh::d_cpolyr (NULL past maxEdges 7)
     const uint32_t* __restrict__ crank;  // mops_mesh::d_cell_rank
@@ -1947,6 +1968,7 @@ __global__ void __launch_bounds__(kTrajBlock, (TrajWaves<MAXV, PATH, EULER, COOP
                     const uint32_t* hdi = reinterpret_cast<const uint32_t*>(s_hdr);
                     const double2* cpoly2 = reinterpret_cast<const double2*>(a.cpoly);
                     const double2* cnrm2 = reinterpret_cast<const double2*>(a.cnrm);
+                    const double2* cedge2 = reinterpret_cast<const double2*>(a.cedge);
                     const double2* pr0 = reinterpret_cast<const double2*>(a.f0.pr);
                     const double2* pr1 = reinterpret_cast<const double2*>(a.f1.pr);
                     // this lane's rank among the live lanes
@@ -1963,9 +1985,11 @@ __global__ void __launch_bounds__(kTrajBlock, (TrajWaves<MAXV, PATH, EULER, COOP
                             const int pp = isn ? 0 : pc - (f1 ? kTileOffRec + kTileRec : kTileOffRec);
                             const int v = pp / (kPairRec / 2), q = pp - (kPairRec / 2) * v;
                             const uint32_t ri = hdi[gg * kTileHdr + 4 + (f1 ? 8 : 0) + v];
-                            const double2* base = isp ? cpoly2 : (isn ? cnrm2 : (f1 ? pr1 : pr0));
+                            const bool ise = MOPS_TILE_E1 && pc >= kTileOffE1;  // (with isn: an edge-vector piece)
+                            const double2* base = isp ? cpoly2 : (isn ? (ise ? cedge2 : cnrm2) : (f1 ? pr1 : pr0));
                             const uint64_t idx = isp ? ((uint64_t)cl * MAXV + (uint32_t)(pc >> 1)) * 2 + (uint32_t)(pc & 1)
-                                                     : (isn ? (uint64_t)cl * kCellNrmPieces + (uint32_t)(pc - kTileOffNrm)
+                                                     : (isn ? (uint64_t)cl * kCellNrmPieces +
+                                                                  (uint32_t)(pc - (ise ? kTileOffE1 : kTileOffNrm))
                                                             : (uint64_t)(ri + (uint32_t)q * pr_qstride((uint32_t)a.V)));
                             s_tile[i] = base[idx];
                         }
@@ -3002,7 +3026,7 @@ __global__ void cpoly_rank_kernel(int64_t C, const int* __restrict__ rank_cell, 
 // cooperative waves' tile takes them from here
 template <int MAXV>
 __global__ void cell_poly_kernel(int64_t C, const int* cellrec, const double4* vxyz, double4* cpoly,
-                                 double* cnrm = nullptr) {
+                                 double* cnrm = nullptr, double* cedge = nullptr) {
     const int64_t c = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (c >= C) return;
     constexpr int REC = ((1 + 2 * MAXV) + 3) / 4 * 4;
@@ -3032,6 +3056,12 @@ __global__ void cell_poly_kernel(int64_t C, const int* cellrec, const double4* v
             o = make_double4(qx, qy, qz, dev::wach_numerator(dev::tri_area(qx, qy, qz, x[i], y[i], z[i], nx, ny, nz)));
         }
         cpoly[c * MAXV + i] = o;
+        if (cedge && 3 * i + 2 < kCellNrm) {  // b - a of the weights' tri_area for slot i (X_{i+1} = poly[i])
+            double* e = cedge + c * kCellNrm + 3 * i;
+            e[0] = i < nv ? x[i] - o.x : 0.0;
+            e[1] = i < nv ? y[i] - o.y : 0.0;
+            e[2] = i < nv ? z[i] - o.z : 0.0;
+        }
         if (cnrm && 3 * i + 2 < kCellNrm) {
             double* n = cnrm + c * kCellNrm + 3 * i;
             if (i < nv) {  // X_i = (qx, qy, qz), X_{i+1} = poly[i] = (x[i], y[i], z[i])
@@ -3044,6 +3074,7 @@ __global__ void cell_poly_kernel(int64_t C, const int* cellrec, const double4* v
         }
     }
     if (cnrm) cnrm[c * kCellNrm + kCellNrm - 1] = 0.0;
+    if (cedge) cedge[c * kCellNrm + kCellNrm - 1] = 0.0;
 }
 
 // Level-pair records (mops_field::d_pr), one 16-B chunk per thread so that a wave's
@@ -3397,7 +3428,7 @@ void free_mesh(mops_mesh* m) {
     if (!m) return;
     (void)hipFree(m->d_cellrec); (void)hipFree(m->d_cxyz); (void)hipFree(m->d_vxyz); (void)hipFree(m->d_cov);
     (void)hipFree(m->d_bary);
-    (void)hipFree(m->d_bkeys); (void)hipFree(m->d_bcells); (void)hipFree(m->d_hkeys); (void)hipFree(m->d_hval); (void)hipFree(m->d_cell_rank); (void)hipFree(m->d_rank_cell); (void)hipFree(m->d_cpolyr); (void)hipFree(m->d_cpoly); (void)hipFree(m->d_cnrm); (void)hipFree(m->d_nbr); (void)hipFree(m->d_rloc2); (void)hipFree(m->d_ring);
+    (void)hipFree(m->d_bkeys); (void)hipFree(m->d_bcells); (void)hipFree(m->d_hkeys); (void)hipFree(m->d_hval); (void)hipFree(m->d_cell_rank); (void)hipFree(m->d_rank_cell); (void)hipFree(m->d_cpolyr); (void)hipFree(m->d_cpoly); (void)hipFree(m->d_cnrm); (void)hipFree(m->d_cedge); (void)hipFree(m->d_nbr); (void)hipFree(m->d_rloc2); (void)hipFree(m->d_ring);
     (void)hipFree(m->d_scratch);
     (void)hipFree(m->d_eoc); (void)hipFree(m->d_coe); (void)hipFree(m->d_exyz); (void)hipFree(m->d_rbf_coef);
     (void)hipFree(m->d_rbf_slot);
@@ -3790,11 +3821,15 @@ mops_status mops_mesh_create(const mops_mesh_desc* desc, void* stream, mops_mesh
                                                         m->d_rloc2, m->d_ring);
     if ((st = dmalloc(&m->d_cpoly, (size_t)(C * m->maxv), &acc)) != MOPS_OK) { free_mesh(m); return st; }
     if (m->maxv == 7 && (st = dmalloc(&m->d_cnrm, (size_t)(C * kCellNrm), &acc)) != MOPS_OK) { free_mesh(m); return st; }
+    if (MOPS_TILE_E1 && m->maxv == 7 && (st = dmalloc(&m->d_cedge, (size_t)(C * kCellNrm), &acc)) != MOPS_OK) {
+        free_mesh(m);
+        return st;
+    }
     if (m->maxv == 7 && (st = dmalloc(&m->d_nbr, (size_t)(C * kNbrQ), &acc)) != MOPS_OK) { free_mesh(m); return st; }
     if (m->maxv == 7) cell_nbr_kernel<<<grid_for(C), kBlock, 0, s>>>(C, m->d_cellrec, m->d_cxyz, m->d_nbr);
     switch (m->maxv) {
         case 7:
-            cell_poly_kernel<7><<<grid_for(C), kBlock, 0, s>>>(C, m->d_cellrec, m->d_vxyz, m->d_cpoly, m->d_cnrm);
+            cell_poly_kernel<7><<<grid_for(C), kBlock, 0, s>>>(C, m->d_cellrec, m->d_vxyz, m->d_cpoly, m->d_cnrm, m->d_cedge);
             if (MOPS_CPOLY_RANK) {
                 if ((st = dmalloc(&m->d_cpolyr, (size_t)(C * 14), &acc)) != MOPS_OK) { free_mesh(m); return st; }
                 cpoly_rank_kernel<<<grid_for(C * 14), kBlock, 0, s>>>(C, m->d_rank_cell, m->d_cpoly, m->d_cpolyr);
@@ -4354,6 +4389,7 @@ mops_status mops_traj_advance(const mops_mesh* mesh, const mops_field* front, co
     a.n_live = p->d_n_live;
     a.cpoly = mesh->d_cpoly;
     a.cnrm = mesh->d_cnrm;
+    a.cedge = mesh->d_cedge;
     a.nbr = mesh->d_nbr;
     a.cpolyr = mesh->d_cpolyr;
     a.crank = mesh->d_cell_rank;

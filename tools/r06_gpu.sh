@@ -38,6 +38,15 @@ rk4ab)  # code-size variants of the tiled RK4 kernel (tools/build_variant.sh noh
   BENCH_ARGS="--method rk4 --steps 1 --warmup 1" OUT=$O/rk4ab ROUNDS=${ROUNDS:-2} bash tools/var_ab.sh base ${RK4_VARIANTS:-nohexprc nohexpr} || exit 11
   cat $O/rk4ab/ab.txt
   ;;
+profile)  # the round's profile of one workload (tools/profile_round.sh: bench, rocprof stats, PMC passes incl. the class mix)
+  bash tools/profile_round.sh $O/${PROF_NAME:-c3} || exit 14
+  grep -h "traj_kernel" $O/${PROF_NAME:-c3}/stats/*kernel_stats.csv | cut -c1-110 | head -4
+  ;;
+stallrk4)
+  BENCH_ARGS="--method rk4" bash tools/pmc_stall.sh $O/stall_rk4 || exit 15
+  python3 tools/pmc_means.py $O/stall_rk4 "void traj_kernel<7, true, false, true>" 240 > $O/stall_rk4/summary.txt
+  tail -8 $O/stall_rk4/summary.txt
+  ;;
 gputests)
   timeout -k 10 1000 python -u -m pytest tests -m gpu -v --maxfail=5 --timeout 300 --timeout-method thread > $O/pytest.log 2>&1
   rc=$?; tail -5 $O/pytest.log; [ $rc -eq 0 ] || exit 6
