@@ -333,6 +333,19 @@ def limiter_text(l1: dict, valu: dict) -> str:
             "issue and gather latency at 3 waves/SIMD (DESIGN.md section 3)")
 
 
+def bench_host() -> str:
+    """This run's box: host name + the GPU's unique id (rocm-smi), as tools/profile_round.sh records the profiled
+    box's (the container host name alone is not unique)."""
+    import subprocess
+    uid = ""
+    try:
+        out = subprocess.run(["rocm-smi", "--showuniqueid"], capture_output=True, text=True, timeout=20).stdout
+        uid = next((ln.split(":")[-1].strip() for ln in out.splitlines() if "unique id" in ln.lower()), "")
+    except (OSError, subprocess.SubprocessError):
+        pass
+    return (socket.gethostname() + " " + uid).strip()
+
+
 def roofline_block(kernel: str, avg_kernel_s: float, psteps_per_launch: float, B: float, traffic_key: str,
                    per: str = "launch") -> dict:
     """The bench line's roofline: HBM GB/s MEASURED by rocprofv3 PMC counters (per launch) over the
@@ -374,7 +387,7 @@ def roofline_block(kernel: str, avg_kernel_s: float, psteps_per_launch: float, B
         "timed_unit": per,
         "particle_steps_per_launch": psteps_per_launch,
         "avg_launch_ms": avg_kernel_s * 1e3,
-        "bench_host": socket.gethostname(),
+        "bench_host": bench_host(),
         # the PMC entry's box and its rocprofv3 launch average: the counters' cycles are that box's, the rate above is
         # this run's (box-to-box spread ~3%)
         "pmc_host": (measured_entry(traffic_key)[0] or {}).get("profile_host"),

@@ -53,8 +53,9 @@ gputests)
   timeout -k 10 300 python -u -c "import __graft_entry__ as g; g.smoke()" > $O/smoke.log 2>&1 || { echo smoke failed; exit 7; }
   tail -1 $O/smoke.log
   ;;
-bench)
-  timeout -k 10 900 python -u bench.py ${BENCH_ARGS:-} > $O/bench.json 2> $O/bench.err || { tail -20 $O/bench.err; exit 8; }
+bench)  # the driver's command (LINE_ARGS, default its --steps 20 --warmup 5); BENCH_ARGS stays the config selection
+  timeout -k 10 900 python -u bench.py ${LINE_ARGS:---steps 20 --warmup 5} ${BENCH_ARGS:-} > $O/bench.json 2> $O/bench.err \
+      || { tail -20 $O/bench.err; exit 8; }
   tail -c 1500 $O/bench.json
   ;;
 esac
