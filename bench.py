@@ -334,16 +334,17 @@ def limiter_text(l1: dict, valu: dict) -> str:
 
 
 def bench_host() -> str:
-    """This run's box: host name + the GPU's unique id (rocm-smi), as tools/profile_round.sh records the profiled
+    """This run's box: host name + the GPU's uuid and PCI address from the device properties (no subprocess: a
+    process that has initialised the GPU must not start programs), as tools/profile_round.sh records the profiled
     box's (the container host name alone is not unique)."""
-    import subprocess
-    uid = ""
+    ident = ""
     try:
-        out = subprocess.run(["rocm-smi", "--showuniqueid"], capture_output=True, text=True, timeout=20).stdout
-        uid = next((ln.split(":")[-1].strip() for ln in out.splitlines() if "unique id" in ln.lower()), "")
-    except (OSError, subprocess.SubprocessError):
+        import torch
+        pr = torch.cuda.get_device_properties(torch.cuda.current_device())
+        ident = f" gpu {pr.uuid} pci {pr.pci_domain_id:04x}:{pr.pci_bus_id:02x}:{pr.pci_device_id:02x}"
+    except Exception:  # (no GPU: the CPU tests)
         pass
-    return (socket.gethostname() + " " + uid).strip()
+    return socket.gethostname() + ident
 
 
 def roofline_block(kernel: str, avg_kernel_s: float, psteps_per_launch: float, B: float, traffic_key: str,

@@ -5,8 +5,8 @@ set -u
 out=${1:-gpurun_out/round}
 mkdir -p "$out"
 export TMPDIR=/tmp
-# the box whose cycles the PMC entry carries (bench.py prints it beside its own): host name + GPU unique id
-{ hostname; rocm-smi --showuniqueid 2>/dev/null | grep -i "unique id" | head -1 | sed 's/.*: *//'; } | paste -sd' ' > "$out/host.txt"
+# the box whose cycles the PMC entry carries (bench.py prints it beside its own): host name + GPU uuid / PCI address
+python3 -c "import bench; print(bench.bench_host())" > "$out/host.txt"
 # the counter passes must see only the measured workload's kernels (bench.py's RK4 companion off)
 export MOPS_BENCH_NO_RK4=1
 timeout -k 10 600 python3 bench.py ${BENCH_ARGS:-} > "$out/bench.json" 2> "$out/bench.err" || { echo "bench failed"; exit 1; }

@@ -47,6 +47,18 @@ stallrk4)
   python3 tools/pmc_means.py $O/stall_rk4 "void traj_kernel<7, true, false, true>" 240 > $O/stall_rk4/summary.txt
   tail -8 $O/stall_rk4/summary.txt
   ;;
+rehearse)  # the N > 1 bench path with both ranks on the one GPU (gloo), default collection (gather to rank 0)
+  MOPS_BENCH_ONE_DEVICE=1 MOPS_BENCH_NO_COMPANIONS=1 timeout -k 10 600 python -u bench.py --gpus 2 --backend gloo --steps 1 \
+      --warmup 0 --pairs 2 --particles 2000000 --no-cpu-baseline > $O/rehearsal_2rank_gloo_root.json \
+      2> $O/rehearsal_2rank_gloo_root.err || { tail -30 $O/rehearsal_2rank_gloo_root.err; exit 16; }
+  tail -c 1200 $O/rehearsal_2rank_gloo_root.json
+  ;;
+configs)  # the other BASELINE configs on the final engine (config 2 call, config 4 30-day run, config 5 year)
+  for c in 2 4 5; do
+    timeout -k 10 700 python -u bench.py --config $c > $O/bench_c$c.json 2> $O/bench_c$c.err || { tail -20 $O/bench_c$c.err; exit 17; }
+    python3 -c "import json; d=json.load(open('$O/bench_c$c.json')); print($c, d['value'], d['ms_per_step'], d['roofline'].get('avg_launch_ms'))"
+  done
+  ;;
 gputests)
   timeout -k 10 1000 python -u -m pytest tests -m gpu -v --maxfail=5 --timeout 300 --timeout-method thread > $O/pytest.log 2>&1
   rc=$?; tail -5 $O/pytest.log; [ $rc -eq 0 ] || exit 6
