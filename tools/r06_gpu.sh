@@ -38,6 +38,10 @@ rk4ab)  # code-size variants of the tiled RK4 kernel (tools/build_variant.sh noh
   BENCH_ARGS="--method rk4 --steps 1 --warmup 1" OUT=$O/rk4ab ROUNDS=${ROUNDS:-2} bash tools/var_ab.sh base ${RK4_VARIANTS:-nohexprc nohexpr} || exit 11
   cat $O/rk4ab/ab.txt
   ;;
+profiles)  # PMC profiles of the other configs' launches (their PMC entries for this engine build)
+  BENCH_ARGS="--config 2" bash tools/profile_round.sh $O/c2 || exit 18
+  BENCH_ARGS="--config 4 --pairs 2" bash tools/profile_round.sh $O/c4 || exit 19
+  ;;
 profile)  # the round's profile of one workload (tools/profile_round.sh: bench, rocprof stats, PMC passes incl. the class mix)
   bash tools/profile_round.sh $O/${PROF_NAME:-c3} || exit 14
   grep -h "traj_kernel" $O/${PROF_NAME:-c3}/stats/*kernel_stats.csv | cut -c1-110 | head -4
