@@ -280,8 +280,22 @@ class RecordGather:
     def _exchange(self, out, inp):
         if self.mode == "all":
             all_gather_flat(self.dist, out, inp, self.backend, self.group)
-        else:
+            return
+        try:
             gather_flat(self.dist, out, inp, self.backend, self.world, self.rank, 0, self.group)
+        except (RuntimeError, NotImplementedError, ValueError) as e:
+            if self.checkpoints > 0 or inp.numel() != 4 * self.stride:  # (only the first exchange: the aux slab)
+                raise
+            # a backend without Gather (it refuses before any byte moves, on every rank alike): fall back to the
+            # all-gather before the first exchange, with every rank's ring allocated
+            import sys
+            print(f"[RecordGather] gather to rank 0 unavailable ({e}); all-gather instead", file=sys.stderr)
+            torch = self.torch
+            self.mode, self.receives = "all", True
+            dev = self.spare.device
+            self.gathered = torch.empty((self.world, self.chunk, 6, self.stride), dtype=torch.float64, device=dev)
+            self.gathered_aux = torch.empty((self.world, 4, self.stride), dtype=torch.float64, device=dev)
+            all_gather_flat(self.dist, self.gathered_aux.view(-1), inp, self.backend, self.group)
 
     def gather_ms(self) -> list:
         """Comm-stream milliseconds of every checkpoint's exchange so far (CUDA; call after synchronize)."""

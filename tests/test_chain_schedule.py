@@ -110,6 +110,13 @@ def _gather_worker(rank, world, port, q, ring_records=1, mode="all"):
     from mops_amd.distributed import RecordGather, max_shard, shard_bounds
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
+    if mode == "rootfail":  # a backend without Gather: RecordGather falls back to the all-gather on every rank
+        from mops_amd import distributed as D
+
+        def _no_gather(*a, **k):
+            raise RuntimeError("gather is not supported by this backend (test)")
+        D.gather_flat = _no_gather
+        mode = "root"
     try:
         mesh = synth.make_mesh(12, n_levels=8)
         snaps = [synth.make_snapshot(mesh, timestep=t, phase=0.35 * t) for t in range(3)]
@@ -153,7 +160,7 @@ def _gather_worker(rank, world, port, q, ring_records=1, mode="all"):
                     pass
             ok &= shard.records is not rec  # the particle set moved to the spare slab
             s_all = np.ascontiguousarray(ref["rec_pos"][:, K - 1])  # continuation points
-        if mode == "root":  # (the ring / chunk checks below are the all-gather path's)
+        if mode == "root" and coll.mode == "root":  # (the ring / chunk checks below are the all-gather path's)
             pl = coll.plan()
             ok &= pl["mode"] == "root" and (pl["received_bytes_per_checkpoint"] > 0) == (rank == 0)
             q.put((rank, bool(ok)))
@@ -191,7 +198,8 @@ def _gather_worker(rank, world, port, q, ring_records=1, mode="all"):
 
 
 @pytest.mark.parametrize("world,ring_records,mode", [(2, 1, "all"), (3, 3, "all"), (4, 1, "all"), (4, 3, "all"),
-                                                     (8, 3, "all"), (8, 1, "root"), (3, 1, "root")])
+                                                     (8, 3, "all"), (8, 1, "root"), (3, 1, "root"),
+                                                     (3, 1, "rootfail")])
 def test_record_gather_gloo_chain_shaped(world, ring_records, mode):
     """Two chained pairs with different record counts: each rank's slot-ordered records, gathered by
     RecordGather and unsharded by the slot ids, equal the single-process (oracle) records bit for bit.
