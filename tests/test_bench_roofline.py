@@ -94,3 +94,17 @@ def test_priced_valu_issue_reconciles_with_valu_busy():
     assert v["frac"] == pytest.approx(v["flat_4_cycle_frac"] * (1 + 3 * 23.1 / 1152.3 + 2.7 / 1152.3), rel=1e-12)
     assert abs(v["frac"] - e["valu_busy"]) < 0.01 < abs(v["flat_4_cycle_frac"] - e["valu_busy"])
     assert bench.VALU_CYC_TRANS_F64 == 16.0 and bench.VALU_CYC_TRANS_F32 == 8.0 and bench.VALU_CYC == 4.0
+
+
+def test_bench_host_starts_no_program(monkeypatch):
+    """The line names its box (host + GPU uuid / PCI address) without starting a program: a process that has
+    initialised the GPU must not exec (round 6 first called rocm-smi, a python script, from the bench)."""
+    import subprocess
+    import bench
+
+    def _refuse(*a, **k):
+        raise AssertionError("bench_host started a program")
+    monkeypatch.setattr(subprocess, "run", _refuse)
+    monkeypatch.setattr(subprocess, "Popen", _refuse)
+    h = bench.bench_host()
+    assert isinstance(h, str) and h

@@ -46,6 +46,11 @@ profile)  # the round's profile of one workload (tools/profile_round.sh: bench, 
   bash tools/profile_round.sh $O/${PROF_NAME:-c3} || exit 14
   grep -h "traj_kernel" $O/${PROF_NAME:-c3}/stats/*kernel_stats.csv | cut -c1-110 | head -4
   ;;
+stalleuler)
+  bash tools/pmc_stall.sh $O/stall_euler || exit 20
+  python3 tools/pmc_means.py $O/stall_euler "void traj_kernel<7, true, true, true>" 1440 > $O/stall_euler/summary.txt
+  tail -8 $O/stall_euler/summary.txt
+  ;;
 stallrk4)
   BENCH_ARGS="--method rk4" bash tools/pmc_stall.sh $O/stall_rk4 || exit 15
   python3 tools/pmc_means.py $O/stall_rk4 "void traj_kernel<7, true, false, true>" 240 > $O/stall_rk4/summary.txt
