@@ -434,6 +434,7 @@ class HostLineSink:
         self.d2h_events = []  # (start, end, bytes) per chunk on the copy stream
         self.pairs = 0
         self._width = {}  # pair -> samples per line (the first pair's K + 1, later pairs K)
+        self._slot_pair = [None, None]  # the pair whose lines each buffer slot holds
 
     def _bufs(self, dev):
         t = self.torch
@@ -446,6 +447,9 @@ class HostLineSink:
 
     def host(self, p: int) -> dict:
         """Pair p's lines on the host (rows in the chain's slot order, ``ids`` = each row's particle)."""
+        if not self.keep_all and self._slot_pair[p % 2] != p:
+            raise ValueError(f"pair {p}'s host lines were overwritten by pair {self._slot_pair[p % 2]} (keep_all=False "
+                             "holds the last two pairs)")
         b = self._pinned[p] if self.keep_all else self.hostbufs[p % 2]
         w = self._width[p]
         return {k: (v if k == "ids" else v[:, :w]) for k, v in b.items()}
@@ -459,11 +463,15 @@ class HostLineSink:
             if self._done[slot] is not None:
                 cs.wait_event(self._done[slot])
             self.pairs += 1
+            self._slot_pair[slot] = p
             if self.keep_all:
                 self._pinned[p] = self._bufs("cpu")
         w = lines["points"].shape[1]
         self._width[p] = w
         lo, hi = self._row, self._row + lines["points"].shape[0]
+        if hi > self.n or w > self.P:
+            raise ValueError(f"HostLineSink sized for {self.n} lines of {self.P} samples: pair {p} hands rows up to {hi} "
+                             f"of {w} samples")
         self._row = hi
         st = self.stage[slot]
         for k, v in lines.items():  # compute stream: device staging (the chain reuses its chunk buffers next)

@@ -147,6 +147,10 @@ def test_host_line_sink_delivers_the_device_lines(ec_pair, keep_all):
             got[ids] = h[k]
             assert torch.equal(got, want[k][:, col].cpu()), (p, k)
     assert torch.equal(res["lastPoint"], want["lastPoint"])
+    with pytest.raises(ValueError):  # sized for 100_002 lines: a bigger chain is refused, not written out of bounds
+        sink(2, {k: torch.zeros((n + 1,) + tuple(v.shape[1:]), dtype=v.dtype, device="cuda")
+                 for k, v in want.items() if k in ("points", "velocity", "temperature", "salinity")},
+             torch.zeros(n + 1, dtype=torch.int32, device="cuda"))
 
 
 def test_record_every_6_minutes_1e7_through_the_hook(ec_pair, oracle_lib):
