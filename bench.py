@@ -749,7 +749,8 @@ def print_prof_counters():
         _lib.load().mops_debug_prof(buf)
         print("prof counters lane-steps, lane walks, lane loads, wave-steps, wave-steps walking, wave-steps loading, "
               "coop wave-steps, coop groups, cells per wave-step (sum), (cell, hint) groups (sum), wave-steps with "
-              "<= 2 cells, with <= 2 groups, wave-steps:", list(buf), file=sys.stderr)
+              "<= 2 cells, with <= 2 groups, wave-steps, lane-steps the neighbour table kept, RK4 hand-offs (waves), of them outside a hexagon:",
+              list(buf), file=sys.stderr)
 
 
 def main_chain(args, mesh, dev, world, rank):

@@ -1553,12 +1553,18 @@ __device__ __forceinline__ bool eval_path(const Cell<MAXV>& c, int L, int V, con
 #ifndef MOPS_HEX_PR_PLAIN
 #define MOPS_HEX_PR_PLAIN 1  // ... and its per-lane evaluation
 #endif
-template <int MAXV, bool PATH, int GR, bool TCHK = false>
+template <int MAXV, bool PATH, int GR, bool TCHK = false, bool HEXTILE = false>
 __device__ __forceinline__ bool eval_at(bool hex, const Cell<MAXV>& c, int L, int V, const Field& f0,
                                         const Field& f1, double px, double py, double pz, double d, double alpha,
                                         int& hint0, int& hint1, double& hx, double& hy, double& hz, double& wv,
                                         bool coop = false, const double2* tile = nullptr, int th0 = 0, int th1 = 0) {
     // (TCHK: the RK4 pathline kernels, four inlined evaluations per step -- code size; see MOPS_HEX_PR_*)
+    // (HEXTILE: the hand-off RK4 kernel, whose waves are all cooperative and hexagonal -- the only instantiation)
+    if constexpr (HEXTILE) {
+        static_assert(MAXV == 7 && PATH, "the hexagon tile evaluation is the MAXV 7 pathline one");
+        return eval_path<MAXV, GR, 6, true, TCHK>(c, L, V, f0, f1, px, py, pz, d, alpha, hint0, hint1, hx, hy, hz, wv,
+                                                  tile, th0, th1);
+    }
     if constexpr (MAXV == 7 && PATH) {
         if (coop) {  // wave-uniform: the tile instantiations
             if ((MOPS_HEX_PR_COOP || !TCHK) && hex) return eval_path<MAXV, GR, 6, true, TCHK>(c, L, V, f0, f1, px, py, pz, d, alpha, hint0, hint1, hx,
@@ -1599,6 +1605,7 @@ struct TrajArgs {
     const uint32_t* __restrict__ crank;  // mops_mesh::d_cell_rank
     const int* __restrict__ coop_sel;   // per-launch device flag: 1 = the cooperative instantiation runs, 0 = the
                                         // plain one (the other exits at once); NULL = no selection
+    int handoff;          // pathline RK4: the hand-off kernel runs first, the cooperative one resumes its waves
     double* px; double* py; double* pz;
     float* depth;
     int* cell;
@@ -1612,6 +1619,28 @@ struct TrajArgs {
     double* rec;
     int64_t rec_stride;
 };
+
+// One piece of a cooperative wave's tile (traj_kernel's regroup): piece pc of group gg -- the polygon, the
+// edge normals, the front field's records, the back field's -- from the group headers hdi into s_tile[i]
+template <int MAXV>
+__device__ __forceinline__ void tile_piece(int i, const uint32_t* hdi, const double2* cpoly2, const double2* cnrm2,
+                                           const double2* cedge2, const double2* pr0, const double2* pr1, uint32_t V,
+                                           double2* s_tile) {
+    const int gg = i / kTilePieces, pc = i - gg * kTilePieces;
+    const uint32_t cl = hdi[gg * kTileHdr];
+    const bool isp = pc < kTileOffNrm, isn = pc < kTileOffRec;
+    const bool f1 = pc >= kTileOffRec + kTileRec;
+    const int pp = isn ? 0 : pc - (f1 ? kTileOffRec + kTileRec : kTileOffRec);
+    const int v = pp / (kPairRec / 2), q = pp - (kPairRec / 2) * v;
+    const uint32_t ri = hdi[gg * kTileHdr + 4 + (f1 ? 8 : 0) + v];
+    const bool ise = MOPS_TILE_E1 && pc >= kTileOffE1;  // (with isn: an edge-vector piece)
+    const double2* base = isp ? cpoly2 : (isn ? (ise ? cedge2 : cnrm2) : (f1 ? pr1 : pr0));
+    const uint64_t idx = isp ? ((uint64_t)cl * MAXV + (uint32_t)(pc >> 1)) * 2 + (uint32_t)(pc & 1)
+                             : (isn ? (uint64_t)cl * kCellNrmPieces +
+                                          (uint32_t)(pc - (ise ? kTileOffE1 : kTileOffNrm))
+                                    : (uint64_t)(ri + (uint32_t)q * pr_qstride(V)));
+    s_tile[i] = base[idx];
+}
 
 // Minimum waves per SIMD requested per instantiation (register budget vs
 // latency hiding; swept on MI355X with tools/occupancy_sweep.sh).
@@ -1696,15 +1725,32 @@ struct LdsNormals {
 #ifndef MOPS_W_PE_PLAIN
 #define MOPS_W_PE_PLAIN MOPS_W_PE  // the plain (not cooperative) pathline Euler kernel
 #endif
-template <int MAXV, bool PATH, bool EULER, bool COOP = false>
+#ifndef MOPS_RK4_HANDOFF
+#define MOPS_RK4_HANDOFF 1  // pathline RK4: a hexagon-tile-only kernel at MOPS_W_PR_HAND waves first (see traj_kernel):
+                            // config-3 RK4 launch 289 vs 313 ms, 7.42e9 vs 6.87e9 p-steps/s (2 interleaved rounds);
+                            // with the tile filled past MOPS_COOP_R pieces per lane there, 287.5 vs 289 ms
+#endif
+#ifndef MOPS_W_PR_HAND
+#define MOPS_W_PR_HAND 3
+#endif
+template <int MAXV, bool PATH, bool EULER, bool COOP = false, bool HAND = false>
 struct TrajWaves {
-    static constexpr int base = PATH ? (EULER ? (COOP ? MOPS_W_PE : MOPS_W_PE_PLAIN) : MOPS_W_PR)
+    static constexpr int base = PATH ? (EULER ? (COOP ? MOPS_W_PE : MOPS_W_PE_PLAIN) : (HAND ? MOPS_W_PR_HAND : MOPS_W_PR))
                                      : (EULER ? MOPS_W_SE : MOPS_W_SR);
     static constexpr int value = MAXV <= 7 ? base : (EULER ? 2 : 1);
 };
 
-template <int MAXV, bool PATH, bool EULER, bool COOP = false>
-__global__ void __launch_bounds__(kTrajBlock, (TrajWaves<MAXV, PATH, EULER, COOP>::value)) traj_kernel(TrajArgs a) {
+// HAND (pathline RK4, MOPS_RK4_HANDOFF): the hand-off kernel.  It holds only the hexagon tile evaluation --
+// the cooperative kernel's other two (the general-polygon tile, the per-lane one) are what keep that kernel at
+// 2 waves/SIMD -- and runs a wave while every step finds it cooperative and hexagonal.  At the first step that
+// does not, the wave stops before the step's walk takes effect and hands over: its state is the step's start
+// (position, depth, the cell the walk starts from) and death[pid] = -2 - step marks where to resume.  The
+// cooperative kernel, launched after it (TrajArgs::handoff), runs only such waves, from that step on: the same
+// as a launch boundary at that step for them (the walk's shortcuts, the hints and the tile are exact or speed
+// only), so records and states are the same bits as one kernel's.
+template <int MAXV, bool PATH, bool EULER, bool COOP = false, bool HAND = false>
+__global__ void __launch_bounds__(kTrajBlock, (TrajWaves<MAXV, PATH, EULER, COOP, HAND>::value)) traj_kernel(TrajArgs a) {
+    static_assert(!HAND || (MAXV == 7 && PATH && !EULER && COOP), "the hand-off kernel is the pathline RK4 tile one");
     if (a.coop_sel && ((*a.coop_sel != 0) != COOP)) return;  // the other instantiation runs this launch
     // XCD-aware mapping: blocks b, b+8, ... share an XCD (L2); give each XCD a
     // contiguous range of the locality-ordered particles (bijective remap)
@@ -1738,10 +1784,19 @@ __global__ void __launch_bounds__(kTrajBlock, (TrajWaves<MAXV, PATH, EULER, COOP
     } stamp_end{stamp};
 #endif
     const int64_t pid = a.order ? (int64_t)a.order[slot] : slot;
+    int64_t sb = a.step_begin;
+    const int dth = a.death[pid];
+    // the cooperative kernel after the hand-off kernel: only the waves it handed over, each from its step (one
+    // per wave: a wave's lanes stop together, and the two kernels map the same slots to a wave)
+    const bool resumed = COOP && !HAND && !EULER && a.handoff;
+    if (resumed) {
+        if (dth > -2) return;  // dead (its records cleared by the hand-off kernel), or finished there
+        sb = (int64_t)__builtin_amdgcn_readfirstlane(-2 - dth);
+    }
     // Records need no initialisation: the launches from step 0 on write every record of every
     // particle -- its samples while alive, then (at its death) the zeros the reference's
     // preallocated trajectory holds (dev::clear_records)
-    if (a.death[pid] >= 0) {  // the reference's lambda has returned
+    if (dth >= 0) {  // the reference's lambda has returned
         if (a.step_begin == 0) dev::clear_records(a.rec, a.rec_stride, pid, 0, a.K);
         return;
     }
@@ -1791,15 +1846,16 @@ __global__ void __launch_bounds__(kTrajBlock, (TrajWaves<MAXV, PATH, EULER, COOP
     // next recording step (the smallest j >= step_begin with (j+1) % rec_period == 0) and its
     // record index, advanced by counting instead of a 64-bit modulo per step
     int64_t rec_next = -1, rec_k = 0;
-    bool rec0 = a.step_begin > 0;  // record 0's step-0 part (seed position, zero velocity) written
+    bool rec0 = sb > 0;  // record 0's step-0 part (seed position, zero velocity) written
     if (a.rec_period > 0) {
-        rec_k = a.step_begin / a.rec_period;
+        rec_k = sb / a.rec_period;
         rec_next = (rec_k + 1) * a.rec_period - 1;
     }
     int tcell = -1, tkey = 0;               // cooperative tile: this lane's (cell, hints) at the last fill + group
     bool have_tile = false, coop_prev = false;  // (wave-uniform)
-    for (int64_t step = a.step_begin; step < a.step_end; ++step) {
+    for (int64_t step = sb; step < a.step_end; ++step) {
         MOPS_MARK(100);
+        [[maybe_unused]] const int cell_in = cell;  // (HAND: the walk restarts from it at a hand-off)
         if (step == 0) {  // first_loop (:892-901)
             if (cell < 0 || cell >= C) { died = 0; break; }
             dev::load_cell<MAXV, kRC, kNrm, kPairT, kCoop>(c, cell, a.cellrec, a.vxyz, a.mono0, a.mono1, a.cxyz, a.cpoly, a.cnrm);
@@ -1893,7 +1949,7 @@ __global__ void __launch_bounds__(kTrajBlock, (TrajWaves<MAXV, PATH, EULER, COOP
             const bool moved = (cell != tcell) | (hk != (tkey & ~0xff));
             // tile mode: regroup when a lane moved; lane-normal mode (a wave with too many groups): try
             // again every 64 steps
-            const bool regroup = c.lds_n ? ((step - a.step_begin) & (MOPS_COOP_RETRY - 1)) == 0
+            const bool regroup = c.lds_n ? ((step - sb) & (MOPS_COOP_RETRY - 1)) == 0
                                          : (__ballot(moved) != 0ull || !have_tile);
             if (regroup) {
                 // groups of live lanes with equal (cell, hint0, hint1), found leader by leader with
@@ -1915,9 +1971,10 @@ __global__ void __launch_bounds__(kTrajBlock, (TrajWaves<MAXV, PATH, EULER, COOP
                     ++G;
                 }
                 // the pieces are spread over the live lanes only (a dead or finished lane has left the
-                // loop): at most MOPS_COOP_R per lane
+                // loop): at most MOPS_COOP_R per lane -- except in the hand-off kernel, which has no other
+                // evaluation and takes the rest in a loop (a wave thinned by deaths, its lanes in different cells)
                 const int nact = __popcll(act);
-                coop = rem == 0ull && G * kTilePieces <= kR * nact &&
+                coop = rem == 0ull && (HAND || G * kTilePieces <= kR * nact) &&
                        (kTileSlots >= MAXV || __ballot(c.nv > kTileSlots) == 0ull);
     #if defined(MOPS_PROF)
                 // [6] cooperative wave-steps, [7] groups of the waves that were grouped in full (rem == 0);
@@ -1977,26 +2034,15 @@ __global__ void __launch_bounds__(kTrajBlock, (TrajWaves<MAXV, PATH, EULER, COOP
     #pragma unroll
                     for (int rr = 0; rr < kR; ++rr) {
                         const int i = rank + nact * rr;
-                        if (i < np) {  // piece pc of group gg: polygon, normals, front records, back records
-                            const int gg = i / kTilePieces, pc = i - gg * kTilePieces;
-                            const uint32_t cl = hdi[gg * kTileHdr];
-                            const bool isp = pc < kTileOffNrm, isn = pc < kTileOffRec;
-                            const bool f1 = pc >= kTileOffRec + kTileRec;
-                            const int pp = isn ? 0 : pc - (f1 ? kTileOffRec + kTileRec : kTileOffRec);
-                            const int v = pp / (kPairRec / 2), q = pp - (kPairRec / 2) * v;
-                            const uint32_t ri = hdi[gg * kTileHdr + 4 + (f1 ? 8 : 0) + v];
-                            const bool ise = MOPS_TILE_E1 && pc >= kTileOffE1;  // (with isn: an edge-vector piece)
-                            const double2* base = isp ? cpoly2 : (isn ? (ise ? cedge2 : cnrm2) : (f1 ? pr1 : pr0));
-                            const uint64_t idx = isp ? ((uint64_t)cl * MAXV + (uint32_t)(pc >> 1)) * 2 + (uint32_t)(pc & 1)
-                                                     : (isn ? (uint64_t)cl * kCellNrmPieces +
-                                                                  (uint32_t)(pc - (ise ? kTileOffE1 : kTileOffNrm))
-                                                            : (uint64_t)(ri + (uint32_t)q * pr_qstride((uint32_t)a.V)));
-                            s_tile[i] = base[idx];
-                        }
+                        if (i < np) tile_piece<MAXV>(i, hdi, cpoly2, cnrm2, cedge2, pr0, pr1, (uint32_t)a.V, s_tile);
+                    }
+                    if constexpr (HAND) {
+                        for (int i = rank + nact * kR; i < np; i += nact)
+                            tile_piece<MAXV>(i, hdi, cpoly2, cnrm2, cedge2, pr0, pr1, (uint32_t)a.V, s_tile);
                     }
                     dev::wave_lds_sync();
                     c.lds_n = false;  // (the tile overwrote the lane normals)
-                } else if (!c.lds_n) {  // tile mode -> lane-normal mode: each lane's normals of its cell
+                } else if (!HAND && !c.lds_n) {  // tile mode -> lane-normal mode: each lane's normals of its cell
 #pragma unroll
                     for (int k = 0; k < 3 * kNrmSlots(MAXV); ++k)
                         c.nrm[k * kTrajBlock] = a.cnrm[(int64_t)cell * kCellNrm + k];
@@ -2011,6 +2057,19 @@ __global__ void __launch_bounds__(kTrajBlock, (TrajWaves<MAXV, PATH, EULER, COOP
                 coop = coop_prev;
             }
             if (coop) tile = s_tile + (tkey & 0xff) * kTilePieces;
+            if constexpr (HAND) {
+                if (!(coop && hex)) {  // hand the wave over at this step (wave-uniform)
+#if defined(MOPS_PROF)
+                    if ((int)__lane_id() == __builtin_ctzll(__ballot(1))) {
+                        atomicAdd(&dev::g_prof[14], 1ull);
+                        if (!hex) atomicAdd(&dev::g_prof[15], 1ull);  // ... of them outside a hexagon
+                    }
+#endif
+                    cell = cell_in;
+                    died = -2 - (int)step;
+                    break;
+                }
+            }
 #if defined(MOPS_PROF)
             if ((int)__lane_id() == __builtin_ctzll(__ballot(1)) && coop) atomicAdd(&dev::g_prof[6], 1ull);
 #endif
@@ -2045,7 +2104,7 @@ __global__ void __launch_bounds__(kTrajBlock, (TrajWaves<MAXV, PATH, EULER, COOP
             for (int stg = 0; stg < 4; ++stg) {
                 double sx, sy, sz, sw;
                 const double as = stg == 0 ? a1 : (stg == 3 ? a4 : a2);
-                ok = dev::eval_at<MAXV, PATH, GR, true>(hex, c, a.L, a.V, a.f0, a.f1, qx, qy, qz, d, as, hint0, hint1,
+                ok = dev::eval_at<MAXV, PATH, GR, true, HAND>(hex, c, a.L, a.V, a.f0, a.f1, qx, qy, qz, d, as, hint0, hint1,
                                                         sx, sy, sz, sw, coop, tile, th0, th1);
                 if (!ok) break;
                 if (stg == 0) {
@@ -2063,48 +2122,48 @@ __global__ void __launch_bounds__(kTrajBlock, (TrajWaves<MAXV, PATH, EULER, COOP
             // The stage velocities summed as they come, in the reference's association ((s1 + 2 s2) + 2 s3) + s4
             // (:959-960): the same operations as the sum at the end, without s1..s3 live across the stages
             double sx, sy, sz, sw, qx, qy, qz;
-            bool ok = dev::eval_at<MAXV, PATH, GR, true>(hex, c, a.L, a.V, a.f0, a.f1, x, y, z, d, a1, hint0, hint1,
+            bool ok = dev::eval_at<MAXV, PATH, GR, true, HAND>(hex, c, a.L, a.V, a.f0, a.f1, x, y, z, d, a1, hint0, hint1,
                                                         sx, sy, sz, sw, coop, tile, th0, th1);
             if (!ok) { died = (int)step; break; }
             hx = sx; hy = sy; hz = sz; wv = sw;
             dev::advect((unsigned)step, x, y, z, sx, sy, sz, dt * 0.5, qx, qy, qz);
             const double a2 = PATH ? dev::dclamp(a1 + 0.5 * a.dalpha, 0.0, 1.0) : 0.0;
             MOPS_STAGE_FENCE();
-            ok = dev::eval_at<MAXV, PATH, GR, true>(hex, c, a.L, a.V, a.f0, a.f1, qx, qy, qz, d, a2, hint0, hint1, sx, sy,
+            ok = dev::eval_at<MAXV, PATH, GR, true, HAND>(hex, c, a.L, a.V, a.f0, a.f1, qx, qy, qz, d, a2, hint0, hint1, sx, sy,
                                                    sz, sw, coop, tile, th0, th1);
             if (!ok) { died = (int)step; break; }
             hx = hx + sx * 2.0; hy = hy + sy * 2.0; hz = hz + sz * 2.0; wv = wv + 2.0 * sw;
             dev::advect((unsigned)step, x, y, z, sx, sy, sz, dt * 0.5, qx, qy, qz);
             MOPS_STAGE_FENCE();
-            ok = dev::eval_at<MAXV, PATH, GR, true>(hex, c, a.L, a.V, a.f0, a.f1, qx, qy, qz, d, a2, hint0, hint1, sx, sy,
+            ok = dev::eval_at<MAXV, PATH, GR, true, HAND>(hex, c, a.L, a.V, a.f0, a.f1, qx, qy, qz, d, a2, hint0, hint1, sx, sy,
                                                    sz, sw, coop, tile, th0, th1);
             if (!ok) { died = (int)step; break; }
             hx = hx + sx * 2.0; hy = hy + sy * 2.0; hz = hz + sz * 2.0; wv = wv + 2.0 * sw;
             dev::advect((unsigned)step, x, y, z, sx, sy, sz, dt, qx, qy, qz);
             const double a4 = PATH ? dev::dclamp(a1 + a.dalpha, 0.0, 1.0) : 0.0;
             MOPS_STAGE_FENCE();
-            ok = dev::eval_at<MAXV, PATH, GR, true>(hex, c, a.L, a.V, a.f0, a.f1, qx, qy, qz, d, a4, hint0, hint1, sx, sy,
+            ok = dev::eval_at<MAXV, PATH, GR, true, HAND>(hex, c, a.L, a.V, a.f0, a.f1, qx, qy, qz, d, a4, hint0, hint1, sx, sy,
                                                    sz, sw, coop, tile, th0, th1);
             if (!ok) { died = (int)step; break; }
             hx = (hx + sx) / 6.0; hy = (hy + sy) / 6.0; hz = (hz + sz) / 6.0; wv = (wv + sw) / 6.0;
 #else
             double s1x, s1y, s1z, s1w, s2x, s2y, s2z, s2w, s3x, s3y, s3z, s3w, s4x, s4y, s4z, s4w;
             double qx, qy, qz;
-            bool ok = dev::eval_at<MAXV, PATH, GR, true>(hex, c, a.L, a.V, a.f0, a.f1, x, y, z, d, a1, hint0, hint1,
+            bool ok = dev::eval_at<MAXV, PATH, GR, true, HAND>(hex, c, a.L, a.V, a.f0, a.f1, x, y, z, d, a1, hint0, hint1,
                                                         s1x, s1y, s1z, s1w, coop, tile, th0, th1);
             if (!ok) { died = (int)step; break; }
             dev::advect((unsigned)step, x, y, z, s1x, s1y, s1z, dt * 0.5, qx, qy, qz);
             const double a2 = PATH ? dev::dclamp(a1 + 0.5 * a.dalpha, 0.0, 1.0) : 0.0;
-            ok = dev::eval_at<MAXV, PATH, GR, true>(hex, c, a.L, a.V, a.f0, a.f1, qx, qy, qz, d, a2, hint0, hint1, s2x,
+            ok = dev::eval_at<MAXV, PATH, GR, true, HAND>(hex, c, a.L, a.V, a.f0, a.f1, qx, qy, qz, d, a2, hint0, hint1, s2x,
                                                    s2y, s2z, s2w, coop, tile, th0, th1);
             if (!ok) { died = (int)step; break; }
             dev::advect((unsigned)step, x, y, z, s2x, s2y, s2z, dt * 0.5, qx, qy, qz);
-            ok = dev::eval_at<MAXV, PATH, GR, true>(hex, c, a.L, a.V, a.f0, a.f1, qx, qy, qz, d, a2, hint0, hint1, s3x,
+            ok = dev::eval_at<MAXV, PATH, GR, true, HAND>(hex, c, a.L, a.V, a.f0, a.f1, qx, qy, qz, d, a2, hint0, hint1, s3x,
                                                    s3y, s3z, s3w, coop, tile, th0, th1);
             if (!ok) { died = (int)step; break; }
             dev::advect((unsigned)step, x, y, z, s3x, s3y, s3z, dt, qx, qy, qz);
             const double a4 = PATH ? dev::dclamp(a1 + a.dalpha, 0.0, 1.0) : 0.0;
-            ok = dev::eval_at<MAXV, PATH, GR, true>(hex, c, a.L, a.V, a.f0, a.f1, qx, qy, qz, d, a4, hint0, hint1, s4x,
+            ok = dev::eval_at<MAXV, PATH, GR, true, HAND>(hex, c, a.L, a.V, a.f0, a.f1, qx, qy, qz, d, a4, hint0, hint1, s4x,
                                                    s4y, s4z, s4w, coop, tile, th0, th1);
             if (!ok) { died = (int)step; break; }
             // (s1 + 2 s2 + 2 s3 + s4) / 6 -- cy::Vec3 operator order (:959-960)
@@ -2159,10 +2218,10 @@ __global__ void __launch_bounds__(kTrajBlock, (TrajWaves<MAXV, PATH, EULER, COOP
     a.px[pid] = x; a.py[pid] = y; a.pz[pid] = z;
     a.depth[pid] = dep;
     a.cell[pid] = cell;
-    if (died >= 0) a.death[pid] = died;
+    if (died != -1 || resumed) a.death[pid] = died;  // (resumed: -1 again unless it died; HAND: -2 - step at a hand-off)
     // slots never sampled: after a death, and past the last record step of a run whose
     // record period does not fill all K slots (streamline recordT % deltaT != 0)
-    if (died >= 0 || a.step_end == a.n_steps) dev::clear_records(a.rec, a.rec_stride, pid, (rec_k == 0 && rec0) ? 1 : rec_k, a.K);
+    if (died >= 0 || (a.step_end == a.n_steps && died == -1)) dev::clear_records(a.rec, a.rec_stride, pid, (rec_k == 0 && rec0) ? 1 : rec_k, a.K);
 }
 
 // the neighbour-table test against the walk it short-cuts (mops_selftest_walk): bit 0 = dev::nbr_stay kept
@@ -3515,6 +3574,7 @@ void launch_traj(const TrajArgs& a, bool path, bool euler, hipStream_t s) {
             traj_kernel<MAXV, true, true><<<g, kTrajBlock, 0, s>>>(a);
         } else {
             if constexpr (MAXV == 7) {
+                if (a.coop_sel && a.handoff) traj_kernel<MAXV, true, false, true, true><<<g, kTrajBlock, 0, s>>>(a);
                 if (a.coop_sel) traj_kernel<MAXV, true, false, true><<<g, kTrajBlock, 0, s>>>(a);
             }
             traj_kernel<MAXV, true, false><<<g, kTrajBlock, 0, s>>>(a);
@@ -4416,6 +4476,7 @@ mops_status mops_traj_advance(const mops_mesh* mesh, const mops_field* front, co
         coop_select_kernel<<<1, 256, 0, s>>>(p->n, p->d_cell, p->d_n_live, sel);
         a.coop_sel = sel;
     }
+    a.handoff = (MOPS_RK4_HANDOFF && !euler && a.coop_sel) ? 1 : 0;
     switch (mesh->maxv) {
         case 7: launch_traj<7>(a, back != nullptr, euler, s); break;
 #if !defined(MOPS_ONLY7)  // experiment builds: MAXV 7 instantiations only

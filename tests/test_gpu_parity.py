@@ -275,15 +275,17 @@ def test_pathline_parity(dev_small, ref_small, small_case, oracle_lib, method):
     print(f"bit-exact points: {exact:.4f}")
 
 
+@pytest.mark.parametrize("method", ["euler", "rk4"])
 @pytest.mark.parametrize("variant", ["forward", "backward", "zlevel"])
-def test_pathline_cooperative_waves(gpu, engine_lib, dev_small, ref_small, small_case, oracle_lib, variant):
-    """Pathline Euler waves that share cells (config 3's density: ~40 particles per cell) take the
+def test_pathline_cooperative_waves(gpu, engine_lib, dev_small, ref_small, small_case, oracle_lib, variant, method):
+    """Pathline waves that share cells (config 3's density: ~40 particles per cell) take the
     cooperative path -- each group's polygon, edge normals and hinted-layer records loaded once into the
-    wave's LDS tile and kept until a lane's cell or layer changes (traj_kernel, MOPS_COOP_PE); waves
-    with more than 7 groups switch to per-lane normals.  Dense cells with one or two depth groups, seeds
-    on land (dead at step 0), particles dying later, a partial last wave; forward, backward (dt < 0),
-    and MPAS z-level columns (partial bottom cells: hint misses change the groups) -- bit-exact
-    against the oracle."""
+    wave's LDS tile and kept until a lane's cell or layer changes (traj_kernel, MOPS_COOP_PE / _PR); waves
+    with more than MOPS_COOP_G groups switch to per-lane normals, and in RK4 (MOPS_RK4_HANDOFF) a wave
+    leaves the hexagon-tile kernel at its first step outside a hexagon or the tile and finishes in the
+    cooperative one.  Dense cells with one or two depth groups, seeds on land (dead at step 0), particles
+    dying later, a partial last wave; forward, backward (dt < 0), and MPAS z-level columns (partial
+    bottom cells: hint misses change the groups) -- bit-exact against the oracle."""
     from mops_amd import synth
     from mops_amd.engine import DeviceField, TrajectoryConfig, run_trajectories
     mesh, _, _ = small_case
@@ -312,14 +314,17 @@ def test_pathline_cooperative_waves(gpu, engine_lib, dev_small, ref_small, small
     seeds.append(land[:37]); depths.append(np.full(37, 500.0))
     seeds = np.concatenate(seeds); depths = np.concatenate(depths).astype(np.float32)
     back = variant == "backward"
-    cfg = TrajectoryConfig(deltaT=120, simulationDuration=43200, recordT=3600, depth=0.0, method=1,
+    euler = method == "euler"
+    cfg = TrajectoryConfig(deltaT=120, simulationDuration=43200, recordT=3600, depth=0.0, method=1 if euler else 0,
                            direction=1 if back else 0)
     got = run_trajectories(dm, f0, f1, cfg, seeds, depths=depths)
     ref = oracle_lib.run(mesh, r0, r1, seeds, depths=depths, delta_t=120, duration=43200, record_t=3600,
-                         euler=True, backward=back, cells=got["cells"])
+                         euler=euler, backward=back, cells=got["cells"])
     assert len(seeds) % 64 != 0
-    assert_lines_match(got, ref, f"pathline cooperative waves ({variant})")
-    assert (ref["death"] >= 0).any() and (ref["death"] < 0).sum() > len(seeds) // 2
+    assert_lines_match(got, ref, f"pathline cooperative waves ({variant}, {method})")
+    assert (ref["death"] >= 0).any() and (ref["death"] < 0).any()
+    if euler:
+        assert (ref["death"] < 0).sum() > len(seeds) // 2
 
 
 def test_record_rules_odd_periods(dev_small, ref_small, small_case, oracle_lib):
