@@ -1784,19 +1784,17 @@ __global__ void __launch_bounds__(kTrajBlock, (TrajWaves<MAXV, PATH, EULER, COOP
     } stamp_end{stamp};
 #endif
     const int64_t pid = a.order ? (int64_t)a.order[slot] : slot;
-    int64_t sb = a.step_begin;
-    const int dth = a.death[pid];
     // the cooperative kernel after the hand-off kernel: only the waves it handed over, each from its step (one
-    // per wave: a wave's lanes stop together, and the two kernels map the same slots to a wave)
+    // per wave: a wave's lanes stop together, and the two kernels map the same slots to a wave); a dead lane's
+    // records were cleared by the hand-off kernel, a finished one is done.  (The register allocation of the Euler
+    // kernel is sensitive to the form of this prologue and of the epilogue: 128 instead of 70 spilled VGPRs.)
     const bool resumed = COOP && !HAND && !EULER && a.handoff;
-    if (resumed) {
-        if (dth > -2) return;  // dead (its records cleared by the hand-off kernel), or finished there
-        sb = (int64_t)__builtin_amdgcn_readfirstlane(-2 - dth);
-    }
+    if (resumed && a.death[pid] > -2) return;
+    const int64_t sb = resumed ? (int64_t)__builtin_amdgcn_readfirstlane(-2 - a.death[pid]) : a.step_begin;
     // Records need no initialisation: the launches from step 0 on write every record of every
     // particle -- its samples while alive, then (at its death) the zeros the reference's
     // preallocated trajectory holds (dev::clear_records)
-    if (dth >= 0) {  // the reference's lambda has returned
+    if (a.death[pid] >= 0) {  // the reference's lambda has returned
         if (a.step_begin == 0) dev::clear_records(a.rec, a.rec_stride, pid, 0, a.K);
         return;
     }
@@ -1851,11 +1849,12 @@ __global__ void __launch_bounds__(kTrajBlock, (TrajWaves<MAXV, PATH, EULER, COOP
         rec_k = sb / a.rec_period;
         rec_next = (rec_k + 1) * a.rec_period - 1;
     }
+    [[maybe_unused]] int cell_in = 0;       // HAND: the cell this step's walk started from
     int tcell = -1, tkey = 0;               // cooperative tile: this lane's (cell, hints) at the last fill + group
     bool have_tile = false, coop_prev = false;  // (wave-uniform)
     for (int64_t step = sb; step < a.step_end; ++step) {
         MOPS_MARK(100);
-        [[maybe_unused]] const int cell_in = cell;  // (HAND: the walk restarts from it at a hand-off)
+        if constexpr (HAND) cell_in = cell;  // (the walk restarts from it at a hand-off)
         if (step == 0) {  // first_loop (:892-901)
             if (cell < 0 || cell >= C) { died = 0; break; }
             dev::load_cell<MAXV, kRC, kNrm, kPairT, kCoop>(c, cell, a.cellrec, a.vxyz, a.mono0, a.mono1, a.cxyz, a.cpoly, a.cnrm);
@@ -2218,10 +2217,19 @@ __global__ void __launch_bounds__(kTrajBlock, (TrajWaves<MAXV, PATH, EULER, COOP
     a.px[pid] = x; a.py[pid] = y; a.pz[pid] = z;
     a.depth[pid] = dep;
     a.cell[pid] = cell;
-    if (died != -1 || resumed) a.death[pid] = died;  // (resumed: -1 again unless it died; HAND: -2 - step at a hand-off)
+    if constexpr (HAND) {
+        if (died != -1) a.death[pid] = died;  // (-2 - step at a hand-off)
+    } else {
+        if (died >= 0 || resumed) a.death[pid] = died;  // (resumed: -1 again unless it died)
+    }
     // slots never sampled: after a death, and past the last record step of a run whose
     // record period does not fill all K slots (streamline recordT % deltaT != 0)
-    if (died >= 0 || (a.step_end == a.n_steps && died == -1)) dev::clear_records(a.rec, a.rec_stride, pid, (rec_k == 0 && rec0) ? 1 : rec_k, a.K);
+    if constexpr (HAND) {
+        if (died >= 0 || (a.step_end == a.n_steps && died == -1))
+            dev::clear_records(a.rec, a.rec_stride, pid, (rec_k == 0 && rec0) ? 1 : rec_k, a.K);
+    } else {
+        if (died >= 0 || a.step_end == a.n_steps) dev::clear_records(a.rec, a.rec_stride, pid, (rec_k == 0 && rec0) ? 1 : rec_k, a.K);
+    }
 }
 
 // the neighbour-table test against the walk it short-cuts (mops_selftest_walk): bit 0 = dev::nbr_stay kept
