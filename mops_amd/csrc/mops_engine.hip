@@ -149,6 +149,11 @@ inline int rec_ints_for(int maxv) { return ((1 + 2 * maxv) + 3) / 4 * 4; }
 #ifndef MOPS_COOP_G_PR
 #define MOPS_COOP_G_PR MOPS_COOP_G  // ... in the RK4 kernel (2 waves/SIMD by VGPRs: LDS to spare)
 #endif
+#ifndef MOPS_COOP_G_PRR
+#define MOPS_COOP_G_PRR 16  // ... in the cooperative RK4 kernel behind the hand-off kernel: the waves handed over
+                            // for more than MOPS_COOP_G_PR groups keep a tile (22 KB LDS, 6 blocks/CU for a tail
+                            // kernel): config-3 RK4 launch 281.8 / 282.0 vs 283.5 / 284.5 ms at 9, 288 at 24
+#endif
 #ifndef MOPS_COOP_R_PR
 #define MOPS_COOP_R_PR MOPS_COOP_R
 #endif
@@ -1827,7 +1832,9 @@ __global__ void __launch_bounds__(kTrajBlock, (TrajWaves<MAXV, PATH, EULER, COOP
     // per-lane edge normals (Cell::nrm); in the cooperative kernel the same LDS holds either them (a wave in
     // lane-normal mode, c.lds_n) or the wave's tile
     // groups per tile and tile pieces per live lane at most (per kernel: the RK4 one has LDS to spare)
-    constexpr int kG = EULER ? MOPS_COOP_G : MOPS_COOP_G_PR, kR = EULER ? MOPS_COOP_R : MOPS_COOP_R_PR;
+    constexpr int kG = EULER ? MOPS_COOP_G : ((HAND || !MOPS_RK4_HANDOFF) ? MOPS_COOP_G_PR : MOPS_COOP_G_PRR),
+                  kR = EULER ? MOPS_COOP_R : MOPS_COOP_R_PR;
+    constexpr bool kFillAll = HAND || (!EULER && MOPS_COOP_G_PRR != MOPS_COOP_G_PR);  // (see the tile fill)
     static_assert(kG <= 254, "group index in tkey's low byte (0xff = no tile)");
     constexpr int kNrmD = 3 * kNrmSlots(MAXV) * kTrajBlock, kTileD = 2 * kG * kTilePieces;
     __shared__ __attribute__((aligned(16))) double s_nrm[kNrm ? (kCoop && kTileD > kNrmD ? kTileD : kNrmD) : 1];
@@ -1973,7 +1980,7 @@ __global__ void __launch_bounds__(kTrajBlock, (TrajWaves<MAXV, PATH, EULER, COOP
                 // loop): at most MOPS_COOP_R per lane -- except in the hand-off kernel, which has no other
                 // evaluation and takes the rest in a loop (a wave thinned by deaths, its lanes in different cells)
                 const int nact = __popcll(act);
-                coop = rem == 0ull && (HAND || G * kTilePieces <= kR * nact) &&
+                coop = rem == 0ull && (kFillAll || G * kTilePieces <= kR * nact) &&
                        (kTileSlots >= MAXV || __ballot(c.nv > kTileSlots) == 0ull);
     #if defined(MOPS_PROF)
                 // [6] cooperative wave-steps, [7] groups of the waves that were grouped in full (rem == 0);
@@ -2035,7 +2042,7 @@ __global__ void __launch_bounds__(kTrajBlock, (TrajWaves<MAXV, PATH, EULER, COOP
                         const int i = rank + nact * rr;
                         if (i < np) tile_piece<MAXV>(i, hdi, cpoly2, cnrm2, cedge2, pr0, pr1, (uint32_t)a.V, s_tile);
                     }
-                    if constexpr (HAND) {
+                    if constexpr (kFillAll) {
                         for (int i = rank + nact * kR; i < np; i += nact)
                             tile_piece<MAXV>(i, hdi, cpoly2, cnrm2, cedge2, pr0, pr1, (uint32_t)a.V, s_tile);
                     }
